@@ -1,0 +1,589 @@
+// Host side of the C ABI (include/blsverify.h): context, HBM workspace, chunked stage pipeline.
+// Every verdict is computed by the device kernels (kernels.h); this file only moves bytes, sequences
+// launches and does the reference's control-flow bookkeeping (share selection order, index parsing).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/blsverify.h"
+#include "../../include/blsverify_testing.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr size_t kMaxChunk = size_t(1) << 20;  // beacons per pipeline pass (~1 GB of staging)
+
+struct DBuf {
+  void* p = nullptr;
+  size_t sz = 0;
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t ensure(size_t need) {
+    if (need <= sz) return hipSuccess;
+    if (p) {
+      (void)hipFree(p);
+      p = nullptr;
+      sz = 0;
+    }
+    size_t want = std::max(need, size_t(256));
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) sz = want;
+    return e;
+  }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+}  // namespace
+
+struct blsv_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // group
+  bool has_group = false;
+  size_t t = 0, n = 0;
+  DBuf commits, commit_inf;
+  // explicit-pk override (verify_messages with pk48)
+  DBuf pk_tab, pk_inf;
+  uint8_t pk_cache[48];
+  bool pk_cache_valid = false;
+  // staging workspace
+  size_t cap = 0;
+  DBuf H, S, F, h_inf, s_inf, cls;
+  // inputs / outputs
+  DBuf in_sigs, in_msgs, in_off, in_len, in_rounds, seeds, bitmap, first_bad, sk, idx, lambdas, scratch, out,
+      pp_tab, pp_inf, sel, g1_cls, misc;
+};
+
+#define HIPCHK(ctx, expr)                                                             \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess) return fail((ctx), BLSV_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+static int fail(blsv_ctx* ctx, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  return code;
+}
+
+static int ensure_workspace(blsv_ctx* c, size_t cnt) {
+  size_t want = std::min(std::max(cnt, size_t(64)), kMaxChunk);
+  want = (want + 63) & ~size_t(63);
+  if (want <= c->cap) return BLSV_OK;
+  HIPCHK(c, c->H.ensure(want * blsk::H_WORDS * 4));
+  HIPCHK(c, c->S.ensure(want * blsk::S_WORDS * 4));
+  HIPCHK(c, c->F.ensure(want * blsk::F_WORDS * 4));
+  HIPCHK(c, c->h_inf.ensure(want));
+  HIPCHK(c, c->s_inf.ensure(want));
+  HIPCHK(c, c->cls.ensure(want));
+  c->cap = want;
+  return BLSV_OK;
+}
+
+// reduce a 32-byte big-endian scalar mod r -> 8 little-endian words
+static void scalar_mod_r(const uint8_t* be32, uint32_t out[8]) {
+  static const uint32_t R[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                                0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* q = be32 + 28 - 4 * i;
+    out[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+  for (int rep = 0; rep < 4; rep++) {  // value < 2^256 < 3r: at most 2 subtractions
+    bool ge = true;
+    for (int i = 7; i >= 0; i--) {
+      if (out[i] != R[i]) {
+        ge = out[i] > R[i];
+        break;
+      }
+    }
+    if (!ge) break;
+    uint64_t br = 0;
+    for (int i = 0; i < 8; i++) {
+      uint64_t d = (uint64_t)out[i] - R[i] - br;
+      out[i] = (uint32_t)d;
+      br = (d >> 63) & 1;
+    }
+  }
+}
+
+// Run stages 2..5 (decompress, miller, final exp, finish) on chunk [base, base + cnt) after
+// the hash stage filled H. pk_mode: 0 = group key / override entry 0, 1 = per-item table.
+struct PkSel {
+  const uint32_t* tab;
+  const uint8_t* inf;
+  const uint32_t* idx;  // nullptr -> entry 0
+};
+
+static int run_tail(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t offset, size_t base, size_t cnt,
+                    const PkSel& pk, uint64_t* d_bitmap, unsigned long long* d_first_bad, uint8_t* d_cls_out,
+                    hipStream_t st) {
+  blsk::launch_decompress_g2(d_sigs, stride, offset, base, cnt, c->S.as<uint32_t>(), c->s_inf.as<uint8_t>(),
+                             c->cls.as<uint8_t>(), st);
+  blsk::launch_miller(pk.tab, pk.inf, pk.idx, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->S.as<uint32_t>(),
+                      c->s_inf.as<uint8_t>(), c->cls.as<uint8_t>(), cnt, c->F.as<uint32_t>(), st);
+  blsk::launch_final_exp(c->F.as<uint32_t>(), cnt, c->cls.as<uint8_t>(), st);
+  blsk::launch_finish(c->cls.as<uint8_t>(), base, cnt, d_bitmap, d_first_bad, st);
+  if (d_cls_out) HIPCHK(c, hipMemcpyAsync(d_cls_out + base, c->cls.p, cnt, hipMemcpyDeviceToDevice, st));
+  HIPCHK(c, hipGetLastError());
+  return BLSV_OK;
+}
+
+static void bitmap_words_to_bytes(const std::vector<uint64_t>& w, size_t n, uint8_t* out) {
+  for (size_t i = 0; i < (n + 7) / 8; i++) {
+    uint8_t b = (uint8_t)(w[i / 8] >> (8 * (i % 8)));
+    if (i == (n + 7) / 8 - 1 && (n % 8)) b &= (uint8_t)((1u << (n % 8)) - 1);
+    out[i] = b;
+  }
+}
+
+// common host-side driver: hash stage chosen by `hash`, signatures already on device
+template <typename HashFn>
+static int verify_driver(blsv_ctx* c, size_t n, const uint8_t* d_sigs, size_t stride, size_t offset, const PkSel& pk,
+                         HashFn hash, uint8_t* ok_bitmap, uint64_t* first_bad_idx, uint8_t* reject_class) {
+  const size_t words = (n + 63) / 64;
+  HIPCHK(c, c->bitmap.ensure(words * 8 + 8));
+  HIPCHK(c, c->first_bad.ensure(8));
+  HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
+  if (reject_class) HIPCHK(c, c->misc.ensure(n + 64));
+  int rc = ensure_workspace(c, n);
+  if (rc) return rc;
+  for (size_t base = 0; base < n; base += c->cap) {
+    const size_t cnt = std::min(c->cap, n - base);
+    hash(base, cnt);
+    rc = run_tail(c, d_sigs, stride, offset, base, cnt, pk, c->bitmap.as<uint64_t>(),
+                  c->first_bad.as<unsigned long long>(), reject_class ? c->misc.as<uint8_t>() : nullptr, c->stream);
+    if (rc) return rc;
+  }
+  std::vector<uint64_t> w(words + 1, 0);
+  uint64_t fb = UINT64_MAX;
+  if (words) HIPCHK(c, hipMemcpyAsync(w.data(), c->bitmap.p, words * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&fb, c->first_bad.p, 8, hipMemcpyDeviceToHost, c->stream));
+  if (reject_class && n) HIPCHK(c, hipMemcpyAsync(reject_class, c->misc.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (ok_bitmap) bitmap_words_to_bytes(w, n, ok_bitmap);
+  if (first_bad_idx) *first_bad_idx = fb;
+  return BLSV_OK;
+}
+
+static PkSel group_pk(blsv_ctx* c) { return {c->commits.as<uint32_t>(), c->commit_inf.as<uint8_t>(), nullptr}; }
+
+// decode one 48-byte G1 point into (tab, inf) entry 0 on device; returns class via *cls
+static int decode_g1(blsv_ctx* c, const uint8_t* pk48, size_t cnt, DBuf& tab, DBuf& inf, std::vector<uint8_t>& cls) {
+  HIPCHK(c, tab.ensure(cnt * blsk::G1_WORDS * 4));
+  HIPCHK(c, inf.ensure(cnt));
+  HIPCHK(c, c->g1_cls.ensure(cnt));
+  HIPCHK(c, c->misc.ensure(cnt * 48));
+  HIPCHK(c, hipMemcpyAsync(c->misc.p, pk48, cnt * 48, hipMemcpyHostToDevice, c->stream));
+  blsk::launch_decompress_g1(c->misc.as<uint8_t>(), cnt, tab.as<uint32_t>(), inf.as<uint8_t>(),
+                             c->g1_cls.as<uint8_t>(), c->stream);
+  HIPCHK(c, hipGetLastError());
+  cls.assign(cnt, 0);
+  HIPCHK(c, hipMemcpyAsync(cls.data(), c->g1_cls.p, cnt, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+// hash of arbitrary messages (packed) on device into H[0..n)
+static int upload_messages(blsv_ctx* c, const uint8_t* msgs, const uint32_t* msg_lens, size_t n) {
+  std::vector<uint64_t> off(n + 1, 0);
+  for (size_t i = 0; i < n; i++) off[i + 1] = off[i] + msg_lens[i];
+  HIPCHK(c, c->in_msgs.ensure(off[n] + 1));
+  HIPCHK(c, c->in_off.ensure((n + 1) * 8));
+  HIPCHK(c, c->in_len.ensure(n * 4 + 4));
+  if (off[n]) HIPCHK(c, hipMemcpyAsync(c->in_msgs.p, msgs, off[n], hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->in_off.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->in_len.p, msg_lens, n * 4, hipMemcpyHostToDevice, c->stream));
+  // keep the host vectors alive until the copies complete
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+extern "C" {
+
+const char* blsv_version(void) { return "drand_amd blsverify 0.1 (gfx950)"; }
+
+int blsv_create(int device, blsv_ctx** out) {
+  if (!out) return BLSV_EINVAL;
+  *out = nullptr;
+  blsv_ctx* c = new blsv_ctx();
+  c->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    fprintf(stderr, "blsv_create: %s\n", hipGetErrorString(e));
+    delete c;
+    return BLSV_EHIP;
+  }
+  *out = c;
+  return BLSV_OK;
+}
+
+void blsv_destroy(blsv_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamDestroy(c->stream);
+  }
+  delete c;
+}
+
+const char* blsv_last_error(const blsv_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int blsv_synchronize(blsv_ctx* c) {
+  if (!c) return BLSV_EINVAL;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+int blsv_set_group(blsv_ctx* c, const uint8_t* commits48, size_t t, size_t n) {
+  if (!c || !commits48 || t == 0 || t > 65536) return fail(c, BLSV_EINVAL, "set_group: bad arguments");
+  (void)hipSetDevice(c->device);
+  std::vector<uint8_t> cls;
+  int rc = decode_g1(c, commits48, t, c->commits, c->commit_inf, cls);
+  if (rc) return rc;
+  for (size_t i = 0; i < t; i++)
+    if (cls[i]) {
+      c->has_group = false;
+      return fail(c, BLSV_EINVAL, "set_group: commitment %zu rejected (class %d)", i, (int)cls[i]);
+    }
+  c->t = t;
+  c->n = n;
+  c->has_group = true;
+  return BLSV_OK;
+}
+
+int blsv_verify_chained(blsv_ctx* c, uint64_t first_round, const uint8_t* prev0, size_t prev0_len,
+                        const uint8_t* sigs96, size_t n, uint8_t* ok_bitmap, uint64_t* first_bad,
+                        uint8_t* reject_class) {
+  if (!c) return BLSV_EINVAL;
+  if (!c->has_group) return fail(c, BLSV_ENOGROUP, "verify_chained: no group key set");
+  if (n && (!sigs96 || !prev0 || (prev0_len != 32 && prev0_len != 96)))
+    return fail(c, BLSV_EINVAL, "verify_chained: prev0 must be 32 or 96 bytes");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, c->in_sigs.ensure(n * 96 + 96));
+  HIPCHK(c, c->seeds.ensure(96));
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, sigs96, n * 96, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->seeds.p, prev0, prev0_len, hipMemcpyHostToDevice, c->stream));
+  }
+  blsk::ChainedSrc src{c->in_sigs.as<uint8_t>(), c->seeds.as<uint8_t>(), first_round, std::max<uint64_t>(n, 1),
+                       (uint32_t)prev0_len};
+  uint64_t fb = UINT64_MAX;
+  int rc = verify_driver(
+      c, n, c->in_sigs.as<uint8_t>(), 96, 0, group_pk(c),
+      [&](size_t base, size_t cnt) {
+        blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
+      },
+      ok_bitmap, &fb, reject_class);
+  if (rc) return rc;
+  if (first_bad) *first_bad = fb == UINT64_MAX ? UINT64_MAX : first_round + fb;
+  return BLSV_OK;
+}
+
+int blsv_verify_unchained(blsv_ctx* c, const uint64_t* rounds, uint64_t first_round, const uint8_t* sigs96, size_t n,
+                          uint8_t* ok_bitmap, uint64_t* first_bad, uint8_t* reject_class) {
+  if (!c) return BLSV_EINVAL;
+  if (!c->has_group) return fail(c, BLSV_ENOGROUP, "verify_unchained: no group key set");
+  if (n && !sigs96) return fail(c, BLSV_EINVAL, "verify_unchained: null signatures");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, c->in_sigs.ensure(n * 96 + 96));
+  if (n) HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, sigs96, n * 96, hipMemcpyHostToDevice, c->stream));
+  const uint64_t* d_rounds = nullptr;
+  if (rounds && n) {
+    HIPCHK(c, c->in_rounds.ensure(n * 8));
+    HIPCHK(c, hipMemcpyAsync(c->in_rounds.p, rounds, n * 8, hipMemcpyHostToDevice, c->stream));
+    d_rounds = c->in_rounds.as<uint64_t>();
+  }
+  uint64_t fb = UINT64_MAX;
+  int rc = verify_driver(
+      c, n, c->in_sigs.as<uint8_t>(), 96, 0, group_pk(c),
+      [&](size_t base, size_t cnt) {
+        blsk::launch_hash_unchained(d_rounds, first_round, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(),
+                                    c->stream);
+      },
+      ok_bitmap, &fb, reject_class);
+  if (rc) return rc;
+  if (first_bad) *first_bad = fb == UINT64_MAX ? UINT64_MAX : (rounds ? rounds[fb] : first_round + fb);
+  return BLSV_OK;
+}
+
+int blsv_verify_messages(blsv_ctx* c, const uint8_t* pk48, const uint8_t* msgs, const uint32_t* msg_lens, size_t n,
+                         const uint8_t* sigs96, uint8_t* ok_bitmap, uint64_t* first_bad, uint8_t* reject_class) {
+  if (!c) return BLSV_EINVAL;
+  if (n && (!msg_lens || !sigs96)) return fail(c, BLSV_EINVAL, "verify_messages: null arguments");
+  (void)hipSetDevice(c->device);
+  PkSel pk;
+  if (pk48) {
+    if (!c->pk_cache_valid || memcmp(c->pk_cache, pk48, 48) != 0) {
+      std::vector<uint8_t> cls;
+      int rc = decode_g1(c, pk48, 1, c->pk_tab, c->pk_inf, cls);
+      if (rc) return rc;
+      if (cls[0]) return fail(c, BLSV_EINVAL, "verify_messages: public key rejected (class %d)", (int)cls[0]);
+      memcpy(c->pk_cache, pk48, 48);
+      c->pk_cache_valid = true;
+    }
+    pk = {c->pk_tab.as<uint32_t>(), c->pk_inf.as<uint8_t>(), nullptr};
+  } else {
+    if (!c->has_group) return fail(c, BLSV_ENOGROUP, "verify_messages: no group key set");
+    pk = group_pk(c);
+  }
+  if (n > kMaxChunk) return fail(c, BLSV_EINVAL, "verify_messages: batch larger than %zu", kMaxChunk);
+  int rc = upload_messages(c, msgs, msg_lens, n);
+  if (rc) return rc;
+  HIPCHK(c, c->in_sigs.ensure(n * 96 + 96));
+  if (n) HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, sigs96, n * 96, hipMemcpyHostToDevice, c->stream));
+  return verify_driver(
+      c, n, c->in_sigs.as<uint8_t>(), 96, 0, pk,
+      [&](size_t base, size_t cnt) {
+        blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>() + base,
+                                   c->in_len.as<uint32_t>() + base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(),
+                                   c->stream);
+      },
+      ok_bitmap, first_bad, reject_class);
+}
+
+// shared by verify_partials / recover: returns per-partial class in cls (host), S staged on device
+static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials,
+                          size_t partial_len, size_t k, std::vector<uint8_t>& cls, std::vector<uint32_t>& index) {
+  cls.assign(k, BLSV_REJ_OK);
+  index.assign(k, 0);
+  if (!c->has_group) return fail(c, BLSV_ENOGROUP, "partials: no group set");
+  if (k > kMaxChunk) return fail(c, BLSV_EINVAL, "partials: too many partials");
+  for (size_t i = 0; i < k; i++) {
+    if (partial_len < 2) {
+      cls[i] = BLSV_REJ_SHARE_INDEX;
+      continue;
+    }
+    const uint8_t* p = partials + i * partial_len;
+    index[i] = ((uint32_t)p[0] << 8) | p[1];
+    if (partial_len != 98) cls[i] = BLSV_REJ_LENGTH;
+  }
+  if (partial_len != 98) return BLSV_OK;  // every share has the wrong signature length
+  int rc = ensure_workspace(c, k);
+  if (rc) return rc;
+  // H(msg) once per item slot (all identical); the per-item PubPoly.Eval(index) table
+  std::vector<uint32_t> lens(k, (uint32_t)msg_len);
+  std::vector<uint8_t> packed;
+  packed.reserve(k * msg_len);
+  for (size_t i = 0; i < k; i++) packed.insert(packed.end(), msg, msg + msg_len);
+  rc = upload_messages(c, packed.data(), lens.data(), k);
+  if (rc) return rc;
+  blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), k,
+                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
+  HIPCHK(c, c->idx.ensure(k * 4));
+  HIPCHK(c, c->pp_tab.ensure(k * blsk::G1_WORDS * 4));
+  HIPCHK(c, c->pp_inf.ensure(k));
+  HIPCHK(c, c->sel.ensure(k * 4));
+  HIPCHK(c, hipMemcpyAsync(c->idx.p, index.data(), k * 4, hipMemcpyHostToDevice, c->stream));
+  std::vector<uint32_t> ident(k);
+  for (size_t i = 0; i < k; i++) ident[i] = (uint32_t)i;
+  HIPCHK(c, hipMemcpyAsync(c->sel.p, ident.data(), k * 4, hipMemcpyHostToDevice, c->stream));
+  blsk::launch_pubpoly_eval(c->commits.as<uint32_t>(), c->commit_inf.as<uint8_t>(), (uint32_t)c->t,
+                            c->idx.as<uint32_t>(), k, c->pp_tab.as<uint32_t>(), c->pp_inf.as<uint8_t>(), c->stream);
+  HIPCHK(c, c->in_sigs.ensure(k * partial_len + 96));
+  HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, partials, k * partial_len, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, c->bitmap.ensure(((k + 63) / 64) * 8 + 8));
+  HIPCHK(c, c->first_bad.ensure(8));
+  HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
+  PkSel pk{c->pp_tab.as<uint32_t>(), c->pp_inf.as<uint8_t>(), c->sel.as<uint32_t>()};
+  rc = run_tail(c, c->in_sigs.as<uint8_t>(), partial_len, 2, 0, k, pk, c->bitmap.as<uint64_t>(),
+                c->first_bad.as<unsigned long long>(), nullptr, c->stream);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(cls.data(), c->cls.p, k, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+int blsv_verify_partials(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
+                         size_t k, uint8_t* ok, uint8_t* reject_class) {
+  if (!c) return BLSV_EINVAL;
+  if (k && (!partials || !ok)) return fail(c, BLSV_EINVAL, "verify_partials: null arguments");
+  (void)hipSetDevice(c->device);
+  std::vector<uint8_t> cls;
+  std::vector<uint32_t> index;
+  int rc = partials_stage(c, msg, msg_len, partials, partial_len, k, cls, index);
+  if (rc) return rc;
+  for (size_t i = 0; i < k; i++) {
+    ok[i] = cls[i] == BLSV_REJ_OK;
+    if (reject_class) reject_class[i] = cls[i];
+  }
+  return BLSV_OK;
+}
+
+int blsv_recover(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
+                 size_t k, size_t t, size_t n, uint8_t* out_sig96) {
+  if (!c) return BLSV_EINVAL;
+  if (!out_sig96 || t == 0 || (k && !partials)) return fail(c, BLSV_EINVAL, "recover: bad arguments");
+  (void)n;
+  (void)hipSetDevice(c->device);
+  std::vector<uint8_t> cls;
+  std::vector<uint32_t> index;
+  int rc = partials_stage(c, msg, msg_len, partials, partial_len, k, cls, index);
+  if (rc) return rc;
+  // first t valid shares in input order, duplicate indices keep the first
+  std::vector<uint32_t> sel, idx;
+  for (size_t i = 0; i < k && sel.size() < t; i++) {
+    if (cls[i] != BLSV_REJ_OK) continue;
+    if (std::find(idx.begin(), idx.end(), index[i]) != idx.end()) continue;
+    sel.push_back((uint32_t)i);
+    idx.push_back(index[i]);
+  }
+  if (sel.size() < t)
+    return fail(c, BLSV_ENOTENOUGH, "share: not enough good public shares to reconstruct secret commitment");
+  HIPCHK(c, c->sel.ensure(t * 4));
+  HIPCHK(c, c->idx.ensure(t * 4));
+  HIPCHK(c, c->lambdas.ensure(t * 32));
+  HIPCHK(c, c->scratch.ensure(t * 72 * 4));
+  HIPCHK(c, c->out.ensure(96));
+  HIPCHK(c, hipMemcpyAsync(c->sel.p, sel.data(), t * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->idx.p, idx.data(), t * 4, hipMemcpyHostToDevice, c->stream));
+  blsk::launch_lagrange(c->idx.as<uint32_t>(), (uint32_t)t, c->lambdas.as<uint32_t>(), c->stream);
+  blsk::launch_recover(c->S.as<uint32_t>(), k, c->s_inf.as<uint8_t>(), c->sel.as<uint32_t>(),
+                       c->lambdas.as<uint32_t>(), (uint32_t)t, c->scratch.as<uint32_t>(), c->out.as<uint8_t>(),
+                       c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out_sig96, c->out.p, 96, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+int blsv_sign(blsv_ctx* c, const uint8_t* sk32, int32_t index, const uint8_t* msgs, const uint32_t* msg_lens, size_t n,
+              uint8_t* out) {
+  if (!c) return BLSV_EINVAL;
+  if (!sk32 || (n && (!msg_lens || !out)) || index > 65535) return fail(c, BLSV_EINVAL, "sign: bad arguments");
+  if (n > kMaxChunk) return fail(c, BLSV_EINVAL, "sign: batch larger than %zu", kMaxChunk);
+  (void)hipSetDevice(c->device);
+  if (!n) return BLSV_OK;
+  uint32_t sk[8];
+  scalar_mod_r(sk32, sk);
+  int rc = ensure_workspace(c, n);
+  if (rc) return rc;
+  rc = upload_messages(c, msgs, msg_lens, n);
+  if (rc) return rc;
+  const size_t stride = index >= 0 ? 98 : 96;
+  HIPCHK(c, c->sk.ensure(32));
+  HIPCHK(c, c->out.ensure(n * stride));
+  HIPCHK(c, hipMemcpyAsync(c->sk.p, sk, 32, hipMemcpyHostToDevice, c->stream));
+  blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), n,
+                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
+  blsk::launch_sign(c->sk.as<uint32_t>(), index, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), n, c->out.as<uint8_t>(),
+                    stride, c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, c->out.p, n * stride, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+int blsv_verify_chained_dev(blsv_ctx* c, uint64_t first_round, uint64_t seg_len, const uint8_t* d_seeds96,
+                            size_t seed0_len, const uint8_t* d_sigs96, size_t n, uint64_t* d_bitmap,
+                            uint64_t* d_first_bad, uint8_t* d_reject_class, void* stream) {
+  if (!c) return BLSV_EINVAL;
+  if (!c->has_group) return fail(c, BLSV_ENOGROUP, "verify_chained_dev: no group key set");
+  if (n && (!d_seeds96 || !d_sigs96 || !d_bitmap || !d_first_bad || (seed0_len != 32 && seed0_len != 96)))
+    return fail(c, BLSV_EINVAL, "verify_chained_dev: bad arguments");
+  (void)hipSetDevice(c->device);
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  HIPCHK(c, hipMemsetAsync(d_first_bad, 0xff, 8, st));
+  int rc = ensure_workspace(c, n);
+  if (rc) return rc;
+  blsk::ChainedSrc src{d_sigs96, d_seeds96, first_round, seg_len ? seg_len : std::max<uint64_t>(n, 1),
+                       (uint32_t)seed0_len};
+  for (size_t base = 0; base < n; base += c->cap) {
+    const size_t cnt = std::min(c->cap, n - base);
+    blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), st);
+    rc = run_tail(c, d_sigs96, 96, 0, base, cnt, group_pk(c), d_bitmap, (unsigned long long*)d_first_bad,
+                  d_reject_class, st);
+    if (rc) return rc;
+  }
+  return BLSV_OK;
+}
+
+int blsv_generate_chained_dev(blsv_ctx* c, const uint8_t* sk32, uint64_t first_round, uint64_t seg_len,
+                              const uint8_t* d_seeds96, size_t seed0_len, uint8_t* d_sigs96, size_t n, void* stream) {
+  if (!c) return BLSV_EINVAL;
+  if (!sk32 || (n && (!d_seeds96 || !d_sigs96)) || (seed0_len != 32 && seed0_len != 96))
+    return fail(c, BLSV_EINVAL, "generate_chained_dev: bad arguments");
+  (void)hipSetDevice(c->device);
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  uint32_t sk[8];
+  scalar_mod_r(sk32, sk);
+  HIPCHK(c, c->sk.ensure(32));
+  HIPCHK(c, hipMemcpyAsync(c->sk.p, sk, 32, hipMemcpyHostToDevice, st));
+  blsk::ChainedSrc src{d_sigs96, d_seeds96, first_round, seg_len ? seg_len : std::max<uint64_t>(n, 1),
+                       (uint32_t)seed0_len};
+  blsk::launch_gen_chained(c->sk.as<uint32_t>(), src, n, d_sigs96, st);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(st));  // sk staging buffer is reused by later calls
+  return BLSV_OK;
+}
+
+// ------------------------------------------------------------------ testing hooks
+int blsv_test_fp_mul(blsv_ctx* c, const uint32_t* a, const uint32_t* b, size_t n, uint32_t* out) {
+  if (!c || (n && (!a || !b || !out))) return BLSV_EINVAL;
+  (void)hipSetDevice(c->device);
+  DBuf da, db, dout;
+  HIPCHK(c, da.ensure(n * 48));
+  HIPCHK(c, db.ensure(n * 48));
+  HIPCHK(c, dout.ensure(n * 48));
+  HIPCHK(c, hipMemcpyAsync(da.p, a, n * 48, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(db.p, b, n * 48, hipMemcpyHostToDevice, c->stream));
+  blsk::launch_test_fp_mul(da.as<uint32_t>(), db.as<uint32_t>(), n, dout.as<uint32_t>(), c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, dout.p, n * 48, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+int blsv_test_pairing(blsv_ctx* c, const uint32_t* p, const uint32_t* q, size_t n, uint32_t* out_f) {
+  if (!c || (n && (!p || !q || !out_f))) return BLSV_EINVAL;
+  (void)hipSetDevice(c->device);
+  DBuf dp, dq, dout;
+  HIPCHK(c, dp.ensure(n * 96));
+  HIPCHK(c, dq.ensure(n * 192));
+  HIPCHK(c, dout.ensure(n * 576));
+  HIPCHK(c, hipMemcpyAsync(dp.p, p, n * 96, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(dq.p, q, n * 192, hipMemcpyHostToDevice, c->stream));
+  blsk::launch_test_pairing(dp.as<uint32_t>(), dq.as<uint32_t>(), n, dout.as<uint32_t>(), c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out_f, dout.p, n * 576, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+int blsv_test_hash_to_g2(blsv_ctx* c, const uint8_t* msgs, const uint32_t* msg_lens, size_t n, uint32_t* out,
+                         uint8_t* inf) {
+  if (!c || (n && (!msg_lens || !out || !inf))) return BLSV_EINVAL;
+  if (n > kMaxChunk) return BLSV_EINVAL;
+  (void)hipSetDevice(c->device);
+  int rc = ensure_workspace(c, n);
+  if (rc) return rc;
+  rc = upload_messages(c, msgs, msg_lens, n);
+  if (rc) return rc;
+  DBuf dout;
+  HIPCHK(c, dout.ensure(n * 192));
+  blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), n,
+                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
+  blsk::launch_test_unpack_g2(c->H.as<uint32_t>(), n, dout.as<uint32_t>(), c->stream);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, dout.p, n * 192, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(inf, c->h_inf.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+}  // extern "C"

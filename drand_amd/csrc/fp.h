@@ -1,0 +1,261 @@
+// Fp arithmetic for BLS12-381 on gfx950: 381-bit prime field, 12 x 32-bit little-endian limbs,
+// Montgomery form (R = 2^384), values kept canonical in [0, p).
+//
+// This is the engine's replacement for kilic/bls12-381's fp.go + the amd64 assembly Montgomery
+// multiply (the [ext] native code on the reference path). Everything above this
+// file (fp2/fp6/fp12, curves, hash-to-curve, pairing) only uses the fp_* API below, so the limb
+// representation can change without touching the tower.
+//
+// Multiplication: CIOS Montgomery with the "no final carry word" simplification, valid because the
+// top limb of p (0x1a0111ea) is < 2^31 - 1 (so t never needs a 13th word). Each limb product is
+// one v_mad_u64_u32 (measured half-rate on gfx950: tools/intrate.hip -> profiles/).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "bls_constants.h"
+
+#define DI __device__ __forceinline__
+
+namespace bls {
+
+struct fp {
+  uint32_t l[12];
+};
+
+DI fp fp_load_const(const uint32_t (&c)[12]) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = c[i];
+  return r;
+}
+
+DI fp fp_zero() {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = 0;
+  return r;
+}
+
+DI fp fp_one() { return fp_load_const(FP_ONE); }
+
+DI bool fp_is_zero(const fp& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) acc |= a.l[i];
+  return acc == 0;
+}
+
+DI bool fp_eq(const fp& a, const fp& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) acc |= a.l[i] ^ b.l[i];
+  return acc == 0;
+}
+
+DI fp fp_select(bool c, const fp& a, const fp& b) {  // c ? a : b
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+
+// r = a - p if a >= p else a, for a < 2p (given as 12 limbs + carry word)
+DI fp fp_reduce_once(const uint32_t (&s)[12], uint32_t carry) {
+  uint32_t d[12];
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(s[i], P_RAW[i], br, &br);
+  // keep s if (carry == 0 and borrow) i.e. s < p
+  bool keep = (carry == 0) & (br != 0);
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = keep ? s[i] : d[i];
+  return r;
+}
+
+DI fp fp_add(const fp& a, const fp& b) {
+  uint32_t s[12];
+  unsigned c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = __builtin_addc(a.l[i], b.l[i], c, &c);
+  return fp_reduce_once(s, c);
+}
+
+DI fp fp_dbl(const fp& a) { return fp_add(a, a); }
+
+DI fp fp_sub(const fp& a, const fp& b) {
+  uint32_t d[12];
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(a.l[i], b.l[i], br, &br);
+  // if borrow, add p back
+  uint32_t m = br ? 0xffffffffu : 0u;
+  unsigned c = 0;
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = __builtin_addc(d[i], P_RAW[i] & m, c, &c);
+  return r;
+}
+
+DI fp fp_neg(const fp& a) {
+  uint32_t d[12];
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(P_RAW[i], a.l[i], br, &br);
+  uint32_t m = fp_is_zero(a) ? 0u : 0xffffffffu;
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = d[i] & m;
+  return r;
+}
+
+// Montgomery product a*b*R^-1 mod p (CIOS, no final carry word).
+// Deliberately NOT inlined: one copy of the 12x12 body per code object keeps kernels small
+// (instruction-cache resident) and compile times sane. Arguments/results are ext_vector u12 so
+// they travel in v0..v23 / v0..v11 (a by-value struct would be passed through scratch), and the
+// body stays within the caller-saved VGPRs so a call costs only the argument moves.
+typedef uint32_t u12 __attribute__((ext_vector_type(12)));
+
+static __device__ __noinline__ u12 fp_mul_u12(u12 a, u12 b) {
+  uint32_t t[12];
+#pragma unroll
+  for (int j = 0; j < 12; j++) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint32_t bi = b[i];
+    uint64_t A = (uint64_t)a[0] * bi + t[0];
+    const uint32_t m = (uint32_t)A * P_INV32;
+    uint64_t C = (uint64_t)m * P_RAW[0] + (uint32_t)A;
+#pragma unroll
+    for (int j = 1; j < 12; j++) {
+      A = (uint64_t)a[j] * bi + t[j] + (A >> 32);
+      C = (uint64_t)m * P_RAW[j] + (uint32_t)A + (C >> 32);
+      t[j - 1] = (uint32_t)C;
+    }
+    t[11] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+  }
+  // conditional subtraction of p
+  uint32_t d[12];
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(t[i], P_RAW[i], br, &br);
+  u12 r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r[i] = br ? t[i] : d[i];
+  return r;
+}
+
+DI u12 fp_to_u12(const fp& a) {
+  u12 v;
+#pragma unroll
+  for (int i = 0; i < 12; i++) v[i] = a.l[i];
+  return v;
+}
+
+DI fp fp_from_u12(const u12& v) {
+  fp a;
+#pragma unroll
+  for (int i = 0; i < 12; i++) a.l[i] = v[i];
+  return a;
+}
+
+DI fp fp_mul(const fp& a, const fp& b) { return fp_from_u12(fp_mul_u12(fp_to_u12(a), fp_to_u12(b))); }
+
+DI fp fp_sqr(const fp& a) { return fp_mul(a, a); }
+
+// small-constant multiples via additions
+DI fp fp_mul3(const fp& a) { return fp_add(fp_dbl(a), a); }
+DI fp fp_mul4(const fp& a) { return fp_dbl(fp_dbl(a)); }
+DI fp fp_mul8(const fp& a) { return fp_dbl(fp_mul4(a)); }
+
+DI fp fp_to_mont(const fp& raw) { return fp_mul(raw, fp_load_const(FP_R2)); }
+
+DI fp fp_from_mont(const fp& a) {
+  fp one = fp_zero();
+  one.l[0] = 1;
+  return fp_mul(a, one);
+}
+
+// a^e for a public exponent given as little-endian 32-bit words (uniform across the wave ->
+// scalar branches, no divergence). Left-to-right 2-bit fixed window: a 4-entry table keeps the
+// caller's VGPR budget small (every kernel that inverts inherits this function's register count).
+template <int NW>
+DI fp fp_pow_words(const fp& a, const uint32_t (&e)[NW]) {
+  const fp a2 = fp_mul(a, a);
+  const fp a3 = fp_mul(a2, a);
+  fp r = fp_one();
+  bool started = false;
+  for (int w = NW - 1; w >= 0; w--) {
+    const uint32_t word = e[w];
+    for (int dig = 15; dig >= 0; dig--) {
+      const uint32_t d = (word >> (2 * dig)) & 3u;
+      if (started) {
+        r = fp_mul(r, r);
+        r = fp_mul(r, r);
+      }
+      if (d) {
+        const fp t = d == 1u ? a : (d == 2u ? a2 : a3);
+        r = started ? fp_mul(r, t) : t;
+        started = true;
+      }
+    }
+  }
+  return r;
+}
+
+static __device__ __noinline__ u12 fp_pow_p_minus_2(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_2)); }
+static __device__ __noinline__ u12 fp_pow_sqrt(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_PLUS_1_DIV_4)); }
+static __device__ __noinline__ u12 fp_pow_legendre(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_1_DIV_2)); }
+
+DI fp fp_inv(const fp& a) { return fp_from_u12(fp_pow_p_minus_2(fp_to_u12(a))); }  // 0 -> 0
+
+// sqrt candidate a^((p+1)/4); caller checks the square
+DI fp fp_sqrt_cand(const fp& a) { return fp_from_u12(fp_pow_sqrt(fp_to_u12(a))); }
+
+// Legendre: true iff a is a non-zero square or zero
+DI bool fp_is_square(const fp& a) {
+  fp l = fp_from_u12(fp_pow_legendre(fp_to_u12(a)));
+  return fp_is_zero(l) || fp_eq(l, fp_one());
+}
+
+// canonical big-endian 48-byte <-> raw limbs (no Montgomery conversion)
+DI fp fp_raw_from_be48(const uint8_t* b) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint8_t* q = b + 44 - 4 * i;
+    r.l[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+  }
+  return r;
+}
+
+DI void fp_raw_to_be48(uint8_t* b, const fp& a) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint8_t* q = b + 44 - 4 * i;
+    q[0] = (uint8_t)(a.l[i] >> 24);
+    q[1] = (uint8_t)(a.l[i] >> 16);
+    q[2] = (uint8_t)(a.l[i] >> 8);
+    q[3] = (uint8_t)a.l[i];
+  }
+}
+
+// raw value < p ?
+DI bool fp_raw_lt_p(const fp& a) {
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) (void)__builtin_subc(a.l[i], P_RAW[i], br, &br);
+  return br != 0;
+}
+
+// raw value > (p-1)/2 ?  (ZCash "lexicographically largest")
+DI bool fp_raw_gt_half(const fp& a) {
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) (void)__builtin_subc(FP_P_MINUS_1_DIV_2_RAW[i], a.l[i], br, &br);
+  return br != 0;  // (p-1)/2 - a < 0
+}
+
+DI bool fp_mont_is_odd(const fp& a) { return fp_from_mont(a).l[0] & 1u; }
+
+}  // namespace bls

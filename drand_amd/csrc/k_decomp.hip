@@ -1,0 +1,60 @@
+// Stage 2: signature decompression (ZCash format) + psi-based G2 subgroup check, and the final
+// verdict reduction (bitmap + first bad index). kilic G2.FromCompressed order [ext].
+#include "kcommon.h"
+
+namespace blsk {
+
+__global__ void __launch_bounds__(TPB) k_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, size_t base,
+                                                       size_t cnt, uint32_t* S, uint8_t* s_inf, uint8_t* cls) {
+  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= cnt) return;
+  uint8_t buf[96];
+  const uint8_t* p = sigs + (base + i) * stride + offset;
+  for (int k = 0; k < 96; k++) buf[k] = p[k];
+  g2a a;
+  bool inf;
+  uint8_t c = g2_decompress(buf, a, inf, true);
+  if (c != REJ_OK) {
+    a.x = fp2_zero();
+    a.y = fp2_zero();
+    inf = true;
+  }
+  st_fp2(S, cnt, i, 0, a.x);
+  st_fp2(S, cnt, i, 2, a.y);
+  s_inf[i] = inf;
+  cls[i] = c;
+}
+
+__global__ void __launch_bounds__(256) k_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap,
+                                                unsigned long long* first_bad) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const bool in = i < cnt;
+  const bool ok = in && cls[i] == REJ_OK;
+  const bool bad = in && !ok;
+  // base is a multiple of 64, so each wave owns one bitmap word
+  const unsigned long long okm = __ballot(ok);
+  const unsigned long long badm = __ballot(bad);
+  const int lane = threadIdx.x & 63;
+  const size_t wave0 = i - lane;
+  if (lane == 0 && wave0 < cnt) {
+    bitmap[(base + wave0) >> 6] = okm;
+    if (badm) atomicMin(first_bad, (unsigned long long)(base + wave0 + __builtin_ctzll(badm)));
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+void launch_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, size_t base, size_t cnt, uint32_t* S,
+                          uint8_t* s_inf, uint8_t* cls, hipStream_t st) {
+  if (!cnt) return;
+  hipLaunchKernelGGL(k_decompress_g2, dim3(grid_for(cnt)), dim3(TPB), 0, st, sigs, stride, offset, base, cnt, S,
+                     s_inf, cls);
+}
+
+void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap, unsigned long long* first_bad,
+                   hipStream_t st) {
+  if (!cnt) return;
+  hipLaunchKernelGGL(k_finish, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, cls, base, cnt, bitmap,
+                     first_bad);
+}
+
+}  // namespace blsk

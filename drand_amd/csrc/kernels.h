@@ -1,0 +1,75 @@
+// Kernel launchers of the beacon-verification engine (host-callable, defined in k_*.hip).
+// Stage pipeline for a batch of beacons (each stage one lane per beacon, SoA staging in HBM):
+//   hash   : message derivation + hash-to-G2            -> H[i]  (affine, 4 Fp slots) + h_inf[i]
+//   decomp : sigma decompression + psi subgroup check    -> S[i]  (affine, 4 Fp slots) + s_inf[i], cls[i]
+//   miller : e(pk_i, H_i) * e(-g1, S_i) multi-Miller loop -> F[i]  (Fp12, 12 Fp slots)
+//   fexp   : final exponentiation, == 1                  -> cls[i] (REJ_PAIRING on mismatch)
+//   finish : verdict bitmap (ballot) + first bad index (atomicMin)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace blsk {
+
+constexpr int H_WORDS = 48;   // affine G2
+constexpr int S_WORDS = 48;   // affine G2
+constexpr int F_WORDS = 144;  // Fp12
+constexpr int G1_WORDS = 24;  // affine G1 (x, y Montgomery), AoS entry in pk tables
+
+// Chained beacons (chain.VerifyBeacon with prev = the previous round's signature): item i has
+// round first_round + i; its prev is seeds[s] (s = i / seg_len, length seed0_len for s == 0 else
+// 96) when i % seg_len == 0, otherwise sigs[i-1]. seg_len = n gives one continuous chain.
+struct ChainedSrc {
+  const uint8_t* sigs;   // n x 96 (global, whole batch)
+  const uint8_t* seeds;  // n_seg x 96 slots
+  uint64_t first_round;
+  uint64_t seg_len;
+  uint32_t seed0_len;  // 32 (genesis GroupHash) or 96
+};
+
+void launch_hash_chained(const ChainedSrc& src, size_t base, size_t cnt, uint32_t* H, uint8_t* h_inf,
+                         hipStream_t st);
+// chain.VerifyBeaconV2: msg = sha256(BE64(round)); rounds == nullptr -> first_round + base + i
+void launch_hash_unchained(const uint64_t* rounds, uint64_t first_round, size_t base, size_t cnt, uint32_t* H,
+                           uint8_t* h_inf, hipStream_t st);
+// arbitrary messages (Scheme.VerifyRecovered / VerifyPartial / Sign): msg i = msgs[off[i] .. off[i]+len[i])
+void launch_hash_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, size_t cnt,
+                          uint32_t* H, uint8_t* h_inf, hipStream_t st);
+// 96-byte compressed signatures at sigs + (base+i)*stride + offset
+void launch_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, size_t base, size_t cnt, uint32_t* S,
+                          uint8_t* s_inf, uint8_t* cls, hipStream_t st);
+// pk for item i: pk_tab[pk_idx ? pk_idx[i] : 0] (G1_WORDS each) with pk_inf flags
+void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
+                   const uint8_t* h_inf, const uint32_t* S, const uint8_t* s_inf, const uint8_t* cls, size_t cnt,
+                   uint32_t* F, hipStream_t st);
+void launch_final_exp(const uint32_t* F, size_t cnt, uint8_t* cls, hipStream_t st);
+// bitmap bit (base+i) = (cls[i] == 0); bitmap must cover whole 64-bit words; first_bad = min index
+void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap, unsigned long long* first_bad,
+                   hipStream_t st);
+
+// ---- group / threshold / signing kernels (k_misc.hip)
+// decompress cnt G1 points (48 B each) -> pk table entries + inf flags + reject class
+void launch_decompress_g1(const uint8_t* in, size_t cnt, uint32_t* tab, uint8_t* inf, uint8_t* cls, hipStream_t st);
+// PubPoly.Eval(idx[i]) over t commits (affine table, none at infinity assumed via inf flags)
+void launch_pubpoly_eval(const uint32_t* commits, const uint8_t* commit_inf, uint32_t t, const uint32_t* idx,
+                         size_t cnt, uint32_t* out_tab, uint8_t* out_inf, hipStream_t st);
+// Lagrange basis at 0 for x_i = idx[i] + 1 over Fr, written as plain 8-word little-endian scalars
+void launch_lagrange(const uint32_t* idx, uint32_t t, uint32_t* lambdas, hipStream_t st);
+// sum_i [lambda_i] S_i over the selected affine staging entries sel[i] (S in SoA of stride n_s),
+// compressed to 96 bytes
+void launch_recover(const uint32_t* S, size_t n_s, const uint8_t* s_inf, const uint32_t* sel, const uint32_t* lambdas,
+                    uint32_t t, uint32_t* scratch, uint8_t* out96, hipStream_t st);
+// signatures: out + i*out_stride (+2 index prefix when index >= 0) = compress(sk * H(msg_i))
+void launch_sign(const uint32_t* sk_words, int32_t index, const uint32_t* H, const uint8_t* h_inf, size_t cnt,
+                 uint8_t* out, size_t out_stride, hipStream_t st);
+// synthetic chained history (client/test/result/mock/result.go:98-132 recipe, per segment):
+// fills sigs (n x 96) for rounds first_round .. first_round+n-1 with the ChainedSrc seed rule
+void launch_gen_chained(const uint32_t* sk_words, const ChainedSrc& src, size_t n, uint8_t* sigs_out, hipStream_t st);
+
+// ---- test hooks (k_misc.hip): raw field / group / pairing building blocks
+void launch_test_fp_mul(const uint32_t* a, const uint32_t* b, size_t cnt, uint32_t* out, hipStream_t st);
+void launch_test_pairing(const uint32_t* p_tab, const uint32_t* q_aff, size_t cnt, uint32_t* out_f, hipStream_t st);
+void launch_test_unpack_g2(const uint32_t* H, size_t cnt, uint32_t* out, hipStream_t st);
+
+}  // namespace blsk

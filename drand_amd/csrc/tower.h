@@ -1,0 +1,220 @@
+// Extension-field tower for BLS12-381 on gfx950, register resident:
+//   Fp2  = Fp[i]  / (i^2 + 1)
+//   Fp6  = Fp2[v] / (v^3 - xi),  xi = 1 + i
+//   Fp12 = Fp6[w] / (w^2 - v)
+// Replaces kilic/bls12-381 fp2.go / fp6.go / fp12.go ([ext]).
+// Element sum_k c_k w^k (k = 0..5) maps to c0 = (c_0, c_2, c_4), c1 = (c_1, c_3, c_5).
+#pragma once
+#include "fp.h"
+
+namespace bls {
+
+struct fp2 {
+  fp c0, c1;
+};
+struct fp6 {
+  fp2 c0, c1, c2;
+};
+struct fp12 {
+  fp6 c0, c1;
+};
+
+// ---------------------------------------------------------------- Fp2
+DI fp2 fp2_load_const(const uint32_t (&c)[2][12]) { return {fp_load_const(c[0]), fp_load_const(c[1])}; }
+DI fp2 fp2_zero() { return {fp_zero(), fp_zero()}; }
+DI fp2 fp2_one() { return {fp_one(), fp_zero()}; }
+DI bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) & fp_is_zero(a.c1); }
+DI bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) & fp_eq(a.c1, b.c1); }
+DI fp2 fp2_select(bool c, const fp2& a, const fp2& b) { return {fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
+DI fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+DI fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+DI fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
+DI fp2 fp2_neg(const fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+DI fp2 fp2_conj(const fp2& a) { return {a.c0, fp_neg(a.c1)}; }
+
+DI fp2 fp2_mul(const fp2& a, const fp2& b) {  // Karatsuba: 3 Fp mul
+  fp t0 = fp_mul(a.c0, b.c0);
+  fp t1 = fp_mul(a.c1, b.c1);
+  fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+
+DI fp2 fp2_sqr(const fp2& a) {  // (a0+a1)(a0-a1), 2 a0 a1: 2 Fp mul
+  fp t = fp_mul(a.c0, a.c1);
+  return {fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(t)};
+}
+
+DI fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
+DI fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1)}; }
+
+// multiply by xi = 1 + i: (a0 - a1) + (a0 + a1) i
+DI fp2 fp2_mul_xi(const fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+
+DI fp2 fp2_inv(const fp2& a) {
+  fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  fp ni = fp_inv(n);
+  return {fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
+}
+
+// ZCash/RFC helpers on Montgomery values
+DI bool fp2_sgn0(const fp2& a) {  // RFC 9380 sgn0 for Fp2
+  fp r0 = fp_from_mont(a.c0);
+  fp r1 = fp_from_mont(a.c1);
+  bool s0 = r0.l[0] & 1u;
+  bool z0 = fp_is_zero(r0);
+  bool s1 = r1.l[0] & 1u;
+  return s0 | (z0 & s1);
+}
+
+DI bool fp2_lex_largest(const fp2& a) {  // ZCash sign bit rule for y
+  fp r1 = fp_from_mont(a.c1);
+  if (!fp_is_zero(r1)) return fp_raw_gt_half(r1);
+  return fp_raw_gt_half(fp_from_mont(a.c0));
+}
+
+// Square root in Fp2 through the norm (p = 3 mod 4), branch-free apart from uniform code:
+//   n = a0^2 + a1^2, s = sqrt(n) in Fp; a' = (a0 + s)/2 (or (a0 - s)/2 if that is 0);
+//   t = a'^((p+1)/4): if t^2 == a' the root is (t, a1/(2t)), else t^2 == -a' and the root is
+//   (a1/(2t), t). Returns false if a is not a square.
+DI bool fp2_sqrt(fp2& out, const fp2& a) {
+  fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  fp s = fp_sqrt_cand(n);
+  bool ok = fp_eq(fp_sqr(s), n);
+  fp inv2 = fp_load_const(FP_INV2);
+  fp ap = fp_mul(fp_add(a.c0, s), inv2);
+  fp am = fp_mul(fp_sub(a.c0, s), inv2);
+  ap = fp_select(fp_is_zero(ap), am, ap);
+  fp t = fp_sqrt_cand(ap);
+  bool direct = fp_eq(fp_sqr(t), ap);
+  fp inv2t = fp_inv(fp_dbl(t));
+  fp other = fp_mul(a.c1, inv2t);
+  fp2 r = {fp_select(direct, t, other), fp_select(direct, other, t)};
+  ok = ok & fp2_eq(fp2_sqr(r), a);
+  out = r;
+  return ok;
+}
+
+DI bool fp2_is_square(const fp2& a) { return fp_is_square(fp_add(fp_sqr(a.c0), fp_sqr(a.c1))); }
+
+// ---------------------------------------------------------------- Fp6
+DI fp6 fp6_zero() { return {fp2_zero(), fp2_zero(), fp2_zero()}; }
+DI fp6 fp6_one() { return {fp2_one(), fp2_zero(), fp2_zero()}; }
+DI fp6 fp6_add(const fp6& a, const fp6& b) { return {fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)}; }
+DI fp6 fp6_sub(const fp6& a, const fp6& b) { return {fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)}; }
+DI fp6 fp6_neg(const fp6& a) { return {fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+DI bool fp6_eq(const fp6& a, const fp6& b) { return fp2_eq(a.c0, b.c0) & fp2_eq(a.c1, b.c1) & fp2_eq(a.c2, b.c2); }
+
+// multiply by v: (a0 + a1 v + a2 v^2) v = xi a2 + a0 v + a1 v^2
+DI fp6 fp6_mul_v(const fp6& a) { return {fp2_mul_xi(a.c2), a.c0, a.c1}; }
+
+DI fp6 fp6_mul(const fp6& a, const fp6& b) {  // Karatsuba, 6 Fp2 mul
+  fp2 t0 = fp2_mul(a.c0, b.c0);
+  fp2 t1 = fp2_mul(a.c1, b.c1);
+  fp2 t2 = fp2_mul(a.c2, b.c2);
+  fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), t1), t2)), t0);
+  fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), t0), t1), fp2_mul_xi(t2));
+  fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), t0), t2), t1);
+  return {c0, c1, c2};
+}
+
+DI fp6 fp6_sqr(const fp6& a) {  // CH-SQR2
+  fp2 s0 = fp2_sqr(a.c0);
+  fp2 ab = fp2_mul(a.c0, a.c1);
+  fp2 s1 = fp2_dbl(ab);
+  fp2 s2 = fp2_sqr(fp2_add(fp2_sub(a.c0, a.c1), a.c2));
+  fp2 bc = fp2_mul(a.c1, a.c2);
+  fp2 s3 = fp2_dbl(bc);
+  fp2 s4 = fp2_sqr(a.c2);
+  fp2 c0 = fp2_add(fp2_mul_xi(s3), s0);
+  fp2 c1 = fp2_add(fp2_mul_xi(s4), s1);
+  fp2 c2 = fp2_sub(fp2_sub(fp2_add(fp2_add(s1, s2), s3), s0), s4);
+  return {c0, c1, c2};
+}
+
+// a * (b0 + b1 v): 5 Fp2 mul
+DI fp6 fp6_mul_by_01(const fp6& a, const fp2& b0, const fp2& b1) {
+  fp2 t0 = fp2_mul(a.c0, b0);
+  fp2 t1 = fp2_mul(a.c1, b1);
+  fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), b1), t1)), t0);
+  fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), t0), t1);
+  fp2 c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), b0), t0), t1);
+  return {c0, c1, c2};
+}
+
+// a * (b1 v): 3 Fp2 mul
+DI fp6 fp6_mul_by_1(const fp6& a, const fp2& b1) {
+  return {fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
+}
+
+DI fp6 fp6_inv(const fp6& a) {
+  fp2 t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  fp2 t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  fp2 t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  fp2 d = fp2_add(fp2_mul(a.c0, t0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, t1), fp2_mul(a.c1, t2))));
+  fp2 di = fp2_inv(d);
+  return {fp2_mul(t0, di), fp2_mul(t1, di), fp2_mul(t2, di)};
+}
+
+// ---------------------------------------------------------------- Fp12
+DI fp12 fp12_one() { return {fp6_one(), fp6_zero()}; }
+DI bool fp12_eq(const fp12& a, const fp12& b) { return fp6_eq(a.c0, b.c0) & fp6_eq(a.c1, b.c1); }
+DI bool fp12_is_one(const fp12& a) { return fp12_eq(a, fp12_one()); }
+DI fp12 fp12_conj(const fp12& a) { return {a.c0, fp6_neg(a.c1)}; }  // a^(p^6)
+
+DI fp12 fp12_mul(const fp12& a, const fp12& b) {  // Karatsuba, 3 Fp6 mul
+  fp6 t0 = fp6_mul(a.c0, b.c0);
+  fp6 t1 = fp6_mul(a.c1, b.c1);
+  fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
+  fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
+  return {c0, c1};
+}
+
+DI fp12 fp12_sqr(const fp12& a) {  // complex squaring, 2 Fp6 mul
+  fp6 ab = fp6_mul(a.c0, a.c1);
+  fp6 t = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  fp6 c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab));
+  fp6 c1 = fp6_add(ab, ab);
+  return {c0, c1};
+}
+
+// f * l where l = (l00 + l01 v) + (l11 v) w  (sparse Miller-loop line, slots 0,1,4): 13 Fp2 mul
+DI fp12 fp12_mul_by_014(const fp12& f, const fp2& l00, const fp2& l01, const fp2& l11) {
+  fp6 a = fp6_mul_by_01(f.c0, l00, l01);
+  fp6 b = fp6_mul_by_1(f.c1, l11);
+  fp6 c = fp6_mul_by_01(fp6_add(f.c0, f.c1), l00, fp2_add(l01, l11));
+  fp6 c1 = fp6_sub(fp6_sub(c, a), b);
+  fp6 c0 = fp6_add(a, fp6_mul_v(b));
+  return {c0, c1};
+}
+
+DI fp12 fp12_inv(const fp12& a) {  // (a0 + a1 w)^-1 = (a0 - a1 w) / (a0^2 - v a1^2)
+  fp6 d = fp6_sub(fp6_sqr(a.c0), fp6_mul_v(fp6_sqr(a.c1)));
+  fp6 di = fp6_inv(d);
+  return {fp6_mul(a.c0, di), fp6_neg(fp6_mul(a.c1, di))};
+}
+
+// Frobenius: (sum c_k w^k)^p = sum conj(c_k) gamma1^k w^k; ^(p^2) = sum c_k gamma2^k w^k.
+// w-power index of each tower slot: c0.c0->0, c1.c0->1, c0.c1->2, c1.c1->3, c0.c2->4, c1.c2->5
+DI fp12 fp12_frob(const fp12& a) {
+  fp12 r;
+  r.c0.c0 = fp2_conj(a.c0.c0);
+  r.c1.c0 = fp2_mul(fp2_conj(a.c1.c0), fp2_load_const(FROB1_GAMMA[1]));
+  r.c0.c1 = fp2_mul(fp2_conj(a.c0.c1), fp2_load_const(FROB1_GAMMA[2]));
+  r.c1.c1 = fp2_mul(fp2_conj(a.c1.c1), fp2_load_const(FROB1_GAMMA[3]));
+  r.c0.c2 = fp2_mul(fp2_conj(a.c0.c2), fp2_load_const(FROB1_GAMMA[4]));
+  r.c1.c2 = fp2_mul(fp2_conj(a.c1.c2), fp2_load_const(FROB1_GAMMA[5]));
+  return r;
+}
+
+DI fp12 fp12_frob2(const fp12& a) {  // gamma2^k lies in Fp
+  fp12 r;
+  r.c0.c0 = a.c0.c0;
+  r.c1.c0 = fp2_mul_fp(a.c1.c0, fp_load_const(FROB2_GAMMA[1][0]));
+  r.c0.c1 = fp2_mul_fp(a.c0.c1, fp_load_const(FROB2_GAMMA[2][0]));
+  r.c1.c1 = fp2_mul_fp(a.c1.c1, fp_load_const(FROB2_GAMMA[3][0]));
+  r.c0.c2 = fp2_mul_fp(a.c0.c2, fp_load_const(FROB2_GAMMA[4][0]));
+  r.c1.c2 = fp2_mul_fp(a.c1.c2, fp_load_const(FROB2_GAMMA[5][0]));
+  return r;
+}
+
+}  // namespace bls

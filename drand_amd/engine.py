@@ -1,0 +1,212 @@
+"""Python handle on one engine context (one HIP device, one stream): thin wrappers over the C ABI.
+
+Every method runs the HIP kernels; nothing here computes a verdict on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+from . import _lib
+from ._lib import u8p, u32p, u64p
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"blsverify error {code}: {msg}")
+        self.code = code
+
+
+@dataclass
+class BatchResult:
+    """Outcome of a batch verify: ok[i] per item, first_bad (round or index, None if all ok),
+    reject classes (REJ_*) per item."""
+    ok: list
+    first_bad: int | None
+    reject_class: list
+
+    @property
+    def all_ok(self):
+        return self.first_bad is None
+
+    def bitmap(self):
+        out = bytearray((len(self.ok) + 7) // 8)
+        for i, v in enumerate(self.ok):
+            if v:
+                out[i // 8] |= 1 << (i % 8)
+        return bytes(out)
+
+
+def _bits(bitmap, n):
+    return [bool(bitmap[i // 8] >> (i % 8) & 1) for i in range(n)]
+
+
+class Engine:
+    """One blsv_ctx. Not thread-safe (like the C context); create one per thread."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = ctypes.c_void_p()
+        rc = self.lib.blsv_create(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise EngineError(rc, f"blsv_create(device={device}) failed")
+        self._h = h
+        self.device = device
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.blsv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc):
+        if rc != 0:
+            raise EngineError(rc, self.lib.blsv_last_error(self._h).decode())
+        return rc
+
+    @property
+    def handle(self):
+        return self._h
+
+    def synchronize(self):
+        self._check(self.lib.blsv_synchronize(self._h))
+
+    # ------------------------------------------------------------------ group
+    def set_group(self, commits, n=None):
+        """commits: list of 48-byte compressed G1 points (commits[0] = group public key)."""
+        commits = [bytes(c) for c in commits]
+        if any(len(c) != 48 for c in commits):
+            raise ValueError("commitments must be 48 bytes")
+        t = len(commits)
+        self._check(self.lib.blsv_set_group(self._h, _lib.buf(b"".join(commits)), t, n if n is not None else t))
+
+    def set_public_key(self, pk48):
+        self.set_group([pk48], 1)
+
+    # ------------------------------------------------------------------ verification
+    def verify_chained(self, first_round, prev0, sigs):
+        n = len(sigs)
+        sigb = b"".join(bytes(s) for s in sigs)
+        if any(len(s) != 96 for s in sigs):
+            raise ValueError("chained signatures must be 96 bytes (reject wrong lengths host-side)")
+        bm = _lib.out_buf((n + 7) // 8)
+        fb = ctypes.c_uint64()
+        cls = _lib.out_buf(n)
+        self._check(self.lib.blsv_verify_chained(self._h, first_round, _lib.buf(prev0), len(prev0), _lib.buf(sigb), n,
+                                                 bm, ctypes.byref(fb), cls))
+        return BatchResult(_bits(bm, n), None if fb.value == 2 ** 64 - 1 else fb.value, list(cls)[:n])
+
+    def verify_unchained(self, sigs, first_round=None, rounds=None):
+        n = len(sigs)
+        if any(len(s) != 96 for s in sigs):
+            raise ValueError("signatures must be 96 bytes (reject wrong lengths host-side)")
+        sigb = b"".join(bytes(s) for s in sigs)
+        rr = None
+        if rounds is not None:
+            rr = (ctypes.c_uint64 * max(n, 1))(*rounds)
+        bm = _lib.out_buf((n + 7) // 8)
+        fb = ctypes.c_uint64()
+        cls = _lib.out_buf(n)
+        self._check(self.lib.blsv_verify_unchained(self._h, rr, first_round or 0, _lib.buf(sigb), n, bm,
+                                                   ctypes.byref(fb), cls))
+        return BatchResult(_bits(bm, n), None if fb.value == 2 ** 64 - 1 else fb.value, list(cls)[:n])
+
+    def verify_messages(self, msgs, sigs, pk48=None):
+        n = len(msgs)
+        assert len(sigs) == n
+        if any(len(s) != 96 for s in sigs):
+            raise ValueError("signatures must be 96 bytes (reject wrong lengths host-side)")
+        lens = (ctypes.c_uint32 * max(n, 1))(*[len(m) for m in msgs])
+        bm = _lib.out_buf((n + 7) // 8)
+        fb = ctypes.c_uint64()
+        cls = _lib.out_buf(n)
+        self._check(self.lib.blsv_verify_messages(self._h, _lib.buf(pk48) if pk48 is not None else None,
+                                                  _lib.buf(b"".join(bytes(m) for m in msgs)), lens, n,
+                                                  _lib.buf(b"".join(bytes(s) for s in sigs)), bm, ctypes.byref(fb),
+                                                  cls))
+        return BatchResult(_bits(bm, n), None if fb.value == 2 ** 64 - 1 else fb.value, list(cls)[:n])
+
+    def verify_partials(self, msg, partials):
+        k = len(partials)
+        plen = len(partials[0]) if k else 98
+        if any(len(p) != plen for p in partials):
+            raise ValueError("partials of one call must share a length")
+        ok = _lib.out_buf(k)
+        cls = _lib.out_buf(k)
+        self._check(self.lib.blsv_verify_partials(self._h, _lib.buf(msg), len(msg),
+                                                  _lib.buf(b"".join(bytes(p) for p in partials)), plen, k, ok, cls))
+        return [bool(x) for x in list(ok)[:k]], list(cls)[:k]
+
+    def recover(self, msg, partials, t, n):
+        k = len(partials)
+        plen = len(partials[0]) if k else 98
+        out = _lib.out_buf(96)
+        self._check(self.lib.blsv_recover(self._h, _lib.buf(msg), len(msg),
+                                          _lib.buf(b"".join(bytes(p) for p in partials)), plen, k, t, n, out))
+        return bytes(out)
+
+    def sign(self, sk32, msgs, index=-1):
+        n = len(msgs)
+        lens = (ctypes.c_uint32 * max(n, 1))(*[len(m) for m in msgs])
+        stride = 98 if index >= 0 else 96
+        out = _lib.out_buf(n * stride)
+        self._check(self.lib.blsv_sign(self._h, _lib.buf(sk32), index, _lib.buf(b"".join(bytes(m) for m in msgs)),
+                                       lens, n, out))
+        ob = bytes(out)
+        return [ob[i * stride:(i + 1) * stride] for i in range(n)]
+
+    # ------------------------------------------------------------------ device-resident batches
+    def verify_chained_dev(self, first_round, seg_len, d_seeds, seed0_len, d_sigs, n, d_bitmap, d_first_bad,
+                           d_cls=None, stream=None):
+        self._check(self.lib.blsv_verify_chained_dev(self._h, first_round, seg_len, d_seeds, seed0_len, d_sigs, n,
+                                                     d_bitmap, d_first_bad, d_cls, stream))
+
+    def generate_chained_dev(self, sk32, first_round, seg_len, d_seeds, seed0_len, d_sigs, n, stream=None):
+        self._check(self.lib.blsv_generate_chained_dev(self._h, _lib.buf(sk32), first_round, seg_len, d_seeds,
+                                                       seed0_len, d_sigs, n, stream))
+
+    # ------------------------------------------------------------------ testing hooks
+    def test_fp_mul(self, a_limbs, b_limbs):
+        n = len(a_limbs) // 12
+        A = (ctypes.c_uint32 * max(len(a_limbs), 1))(*a_limbs)
+        B = (ctypes.c_uint32 * max(len(b_limbs), 1))(*b_limbs)
+        O = (ctypes.c_uint32 * max(n * 12, 1))()
+        self._check(self.lib.blsv_test_fp_mul(self._h, A, B, n, O))
+        return list(O)[:n * 12]
+
+    def test_pairing(self, p_words, q_words):
+        n = len(p_words) // 24
+        Pp = (ctypes.c_uint32 * max(len(p_words), 1))(*p_words)
+        Q = (ctypes.c_uint32 * max(len(q_words), 1))(*q_words)
+        O = (ctypes.c_uint32 * max(n * 144, 1))()
+        self._check(self.lib.blsv_test_pairing(self._h, Pp, Q, n, O))
+        return list(O)[:n * 144]
+
+    def test_hash_to_g2(self, msgs):
+        n = len(msgs)
+        lens = (ctypes.c_uint32 * max(n, 1))(*[len(m) for m in msgs])
+        O = (ctypes.c_uint32 * max(n * 48, 1))()
+        inf = _lib.out_buf(n)
+        self._check(self.lib.blsv_test_hash_to_g2(self._h, _lib.buf(b"".join(bytes(m) for m in msgs)), lens, n, O,
+                                                  inf))
+        return list(O)[:n * 48], list(inf)[:n]
+
+
+def limbs_of(v, n=12):
+    return [(v >> (32 * i)) & 0xFFFFFFFF for i in range(n)]
+
+
+def int_of(limbs):
+    return sum(int(x) << (32 * i) for i, x in enumerate(limbs))

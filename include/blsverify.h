@@ -1,0 +1,157 @@
+/*
+ * blsverify.h -- C ABI of the MI355X-native BLS12-381 beacon-verification engine.
+ *
+ * This is the drop-in boundary for drand's verification hot path. The reference
+ * calls five methods on the package-level `key.Scheme` (tbls.NewThresholdSchemeOnG2(Pairing),
+ * key/curve.go:31) plus the chain entry points built on it; each entry point below names the
+ * reference interface it replaces. A cgo package (gpu/blsverify) binds these
+ * symbols one-to-one.
+ *
+ * Conventions
+ *  - All buffers are caller-owned host memory valid only for the duration of the call (cgo rules);
+ *    the library copies into HBM and never retains caller pointers. The *_dev entry points take
+ *    device pointers (HBM-resident batches, used by bench.py and multi-GPU sharding).
+ *  - Return value: 0 = the call succeeded (per-item verdicts are in the outputs); < 0 =
+ *    infrastructure error (bad arguments, HIP failure); details from blsv_last_error().
+ *  - Accept/reject and recovered signature bytes are bit-exact with the reference kyber path;
+ *    the optional reject_class output explains a reject (BLSV_REJ_*), error text is not graded.
+ *  - Bitmaps: bit i (byte i/8, bit i%8, LSB first) = 1 iff item i verified.
+ *  - first_bad: the ROUND number (chained/unchained) or the INDEX (message batches) of the first
+ *    rejected item, UINT64_MAX when every item verified.
+ *  - A context owns one HIP stream and is not thread-safe; use one context per calling thread
+ *    (the Go adapter serialises with a mutex or keeps a pool).
+ */
+#ifndef DRAND_AMD_BLSVERIFY_H
+#define DRAND_AMD_BLSVERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct blsv_ctx blsv_ctx;
+
+/* return codes */
+#define BLSV_OK 0
+#define BLSV_EINVAL (-1)
+#define BLSV_EHIP (-2)
+#define BLSV_ENOGROUP (-3)
+#define BLSV_ENOTENOUGH (-4) /* Recover: fewer than t valid shares */
+
+/* reject classes (per item) -- the order of kilic G2.FromCompressed's checks, then the pairing */
+#define BLSV_REJ_OK 0
+#define BLSV_REJ_LENGTH 1          /* wrong byte length (host-side)                      */
+#define BLSV_REJ_FLAG 2            /* compression bit 0x80 clear                          */
+#define BLSV_REJ_INF_NONZERO 3     /* infinity bit set but not exactly 0xc0 || 0...       */
+#define BLSV_REJ_X_GE_P 4          /* a coordinate limb >= p                              */
+#define BLSV_REJ_NOT_ON_CURVE 5    /* x^3 + b has no square root                          */
+#define BLSV_REJ_NOT_IN_SUBGROUP 6 /* point not in the order-r subgroup                   */
+#define BLSV_REJ_PAIRING 7         /* "bls: invalid signature" (pairing check failed)     */
+#define BLSV_REJ_SHARE_INDEX 8     /* tbls share shorter than its 2-byte index prefix     */
+
+#define BLSV_SIG_LEN 96
+#define BLSV_PARTIAL_LEN 98
+#define BLSV_PK_LEN 48
+
+/* Library version string. */
+const char* blsv_version(void);
+
+/* Create a context on HIP device `device`. */
+int blsv_create(int device, blsv_ctx** out);
+void blsv_destroy(blsv_ctx* ctx);
+/* Last error message of this context ("" if none). */
+const char* blsv_last_error(const blsv_ctx* ctx);
+
+/*
+ * Group state: the distributed public polynomial commitments (key.Share.PubPoly /
+ * DistPublic.PubPoly, key/keys.go:235-241,316-324), t commitments of 48 bytes; the group public
+ * key is commits[0] (DistPublic.Key(), chain.Info.PublicKey, chain/info.go:16-21). n is the group
+ * size passed to Recover. A single-key chain is t = 1. Decoding follows kilic G1.FromCompressed
+ * (chain/convert.go:15-18); returns BLSV_EINVAL if any commitment fails to decode.
+ */
+int blsv_set_group(blsv_ctx* ctx, const uint8_t* commits48, size_t t, size_t n);
+
+/*
+ * chain.VerifyBeacon (chain/beacon.go:87-92) over a contiguous chained range: beacon i has round
+ * first_round + i, signature sigs96[i], and PreviousSig = prev0 (i == 0; 32 bytes = genesis seed
+ * GroupHash at round 1, client/verify.go:122-124, or 96 bytes) or sigs96[i-1]. Replaces the serial
+ * walk of client/verify.go:146-163 and chain/beacon/sync.go:100-119 with one batched call.
+ * reject_class (optional, n bytes) receives BLSV_REJ_* per beacon.
+ */
+int blsv_verify_chained(blsv_ctx* ctx, uint64_t first_round, const uint8_t* prev0, size_t prev0_len,
+                        const uint8_t* sigs96, size_t n, uint8_t* ok_bitmap, uint64_t* first_bad,
+                        uint8_t* reject_class);
+
+/*
+ * chain.VerifyBeaconV2 (chain/beacon.go:94-98): msg = sha256(BE64(round)) over SignatureV2.
+ * rounds may be NULL (then round i = first_round + i).
+ */
+int blsv_verify_unchained(blsv_ctx* ctx, const uint64_t* rounds, uint64_t first_round, const uint8_t* sigs96,
+                          size_t n, uint8_t* ok_bitmap, uint64_t* first_bad, uint8_t* reject_class);
+
+/*
+ * key.Scheme.VerifyRecovered(pub, msg, sig) (chain/beacon.go:91, chain/beacon/chain.go:141,162) and
+ * key.AuthScheme.Verify (key/keys.go:60-63) in batch form: message i is msgs[off_i .. off_i+len_i)
+ * with msg_lens[i] bytes (consecutive), verified against pk48 (NULL = group key) and sigs96[i].
+ * first_bad receives the index of the first reject.
+ */
+int blsv_verify_messages(blsv_ctx* ctx, const uint8_t* pk48, const uint8_t* msgs, const uint32_t* msg_lens,
+                         size_t n, const uint8_t* sigs96, uint8_t* ok_bitmap, uint64_t* first_bad,
+                         uint8_t* reject_class);
+
+/*
+ * key.Scheme.VerifyPartial(pubPoly, msg, partial) (chain/beacon/node.go:112,125) for k partials of
+ * partial_len bytes each (98 = 2-byte BE share index || 96-byte signature); all share H(msg).
+ * ok[i] = 1/0; reject_class optional.
+ */
+int blsv_verify_partials(blsv_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8_t* partials,
+                         size_t partial_len, size_t k, uint8_t* ok, uint8_t* reject_class);
+
+/*
+ * key.Scheme.Recover(pubPoly, msg, sigs, t, n) (chain/beacon/chain.go:136,155): verifies the
+ * partials, keeps the first t valid ones in input order (duplicate indices keep the first),
+ * Lagrange-interpolates sum lambda_i sigma_i at 0 over x = index + 1 and writes the compressed
+ * 96-byte group signature. Returns BLSV_ENOTENOUGH with fewer than t valid shares.
+ */
+int blsv_recover(blsv_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
+                 size_t k, size_t t, size_t n, uint8_t* out_sig96);
+
+/*
+ * key.Scheme.Sign(priShare, msg) (chain/beacon/crypto.go:58) / AuthScheme.Sign in batch form:
+ * out[i] = (index >= 0 ? BE16(index) : "") || compress(sk * H(msg_i)); sk32 is the big-endian
+ * scalar (kyber Scalar.MarshalBinary), reduced mod r. Output stride 98 with index, 96 without.
+ */
+int blsv_sign(blsv_ctx* ctx, const uint8_t* sk32, int32_t index, const uint8_t* msgs, const uint32_t* msg_lens,
+              size_t n, uint8_t* out);
+
+/* ---------------------------------------------------------------- device-resident batches */
+
+/*
+ * Chained verify over HBM-resident signatures, optionally split into independently seeded
+ * segments of seg_len rounds (seg_len = 0 means one segment): beacon i (round first_round + i)
+ * uses d_seeds96[s] as PreviousSig when i = s * seg_len (length seed0_len for s = 0, else 96),
+ * else d_sigs96[i-1]. Outputs (device): d_bitmap (ceil(n/64) uint64 words, fully written),
+ * d_first_bad (one uint64: the ROUND of the first reject or UINT64_MAX), d_reject_class (optional,
+ * n bytes). Asynchronous on `stream` (a hipStream_t; NULL = the context stream).
+ */
+int blsv_verify_chained_dev(blsv_ctx* ctx, uint64_t first_round, uint64_t seg_len, const uint8_t* d_seeds96,
+                            size_t seed0_len, const uint8_t* d_sigs96, size_t n, uint64_t* d_bitmap,
+                            uint64_t* d_first_bad, uint8_t* d_reject_class, void* stream);
+
+/*
+ * Synthetic chained history (client/test/result/mock/result.go:98-132, per segment, on device):
+ * d_sigs96[i] = compress(sk * H(Message(first_round + i, prev))) with the seed rule above.
+ */
+int blsv_generate_chained_dev(blsv_ctx* ctx, const uint8_t* sk32, uint64_t first_round, uint64_t seg_len,
+                              const uint8_t* d_seeds96, size_t seed0_len, uint8_t* d_sigs96, size_t n, void* stream);
+
+/* Wait for the context stream. */
+int blsv_synchronize(blsv_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DRAND_AMD_BLSVERIFY_H */

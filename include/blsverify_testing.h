@@ -1,0 +1,33 @@
+/*
+ * blsverify_testing.h -- building-block entry points used only by the parity tests (tests/) to
+ * check the device field and pairing arithmetic against the CPU oracle. Not part of the drop-in
+ * boundary; exported by the same shared library.
+ */
+#ifndef DRAND_AMD_BLSVERIFY_TESTING_H
+#define DRAND_AMD_BLSVERIFY_TESTING_H
+
+#include "blsverify.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* out[i] = a[i] * b[i] mod p; 12 little-endian u32 limbs per element, canonical (< p) inputs. */
+int blsv_test_fp_mul(blsv_ctx* ctx, const uint32_t* a, const uint32_t* b, size_t n, uint32_t* out);
+
+/*
+ * out_f[i] = e(P_i, Q_i)^3 (the engine's reduced pairing is the cube of the textbook value), as 144
+ * u32 words: 12 Fp values (12 limbs each) in tower order c0.c0.{c0,c1}, c0.c1.{..}, c0.c2, c1.c0,
+ * c1.c1, c1.c2. P: 24 words (x, y); Q: 48 words (x.c0, x.c1, y.c0, y.c1); raw (non-Montgomery).
+ */
+int blsv_test_pairing(blsv_ctx* ctx, const uint32_t* p, const uint32_t* q, size_t n, uint32_t* out_f);
+
+/* out[i] = H(msg_i) as affine raw words (x.c0, x.c1, y.c0, y.c1; 48 words) + inf flag. */
+int blsv_test_hash_to_g2(blsv_ctx* ctx, const uint8_t* msgs, const uint32_t* msg_lens, size_t n, uint32_t* out,
+                         uint8_t* inf);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

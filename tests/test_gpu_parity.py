@@ -1,0 +1,133 @@
+"""GPU parity tests: the HIP engine (through the C ABI) against the CPU oracle and the golden
+fixtures. Bit-exact for every integer/byte result (accept/reject, reject class, signature bytes).
+
+Run on an MI355X: python -u -m pytest -x -v -m gpu --timeout 120 --timeout-method thread
+"""
+import random
+
+import pytest
+
+from oracle import bls12381 as O
+
+pytestmark = pytest.mark.gpu
+
+
+def limbs(v):
+    return [(v >> (32 * i)) & 0xFFFFFFFF for i in range(12)]
+
+
+def from_limbs(ws):
+    return sum(int(w) << (32 * i) for i, w in enumerate(ws))
+
+
+# ------------------------------------------------------------------ building blocks
+def test_fp_mul_random(engine):
+    rng = random.Random(1)
+    vals = [0, 1, 2, O.P - 1, O.P - 2, (O.P - 1) // 2] + [rng.randrange(O.P) for _ in range(250)]
+    a = vals
+    b = list(reversed(vals))
+    A = sum((limbs(x) for x in a), [])
+    B = sum((limbs(x) for x in b), [])
+    out = engine.test_fp_mul(A, B)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert from_limbs(out[12 * i:12 * i + 12]) == x * y % O.P, i
+
+
+def test_hash_to_g2_golden(engine, golden):
+    vecs = golden["hash_to_g2"]
+    msgs = [bytes.fromhex(v["msg"]) for v in vecs]
+    out, inf = engine.test_hash_to_g2(msgs)
+    for i, v in enumerate(vecs):
+        got = [from_limbs(out[48 * i + 12 * s:48 * i + 12 * s + 12]) for s in range(4)]
+        want = [int(v["x"][0], 16), int(v["x"][1], 16), int(v["y"][0], 16), int(v["y"][1], 16)]
+        assert inf[i] == 0
+        assert got == want, f"hash_to_g2 mismatch for msg {v['msg'][:16]}"
+
+
+def test_pairing_golden(engine, golden):
+    """Engine reduced pairing = e(P, Q)^3 (hard part uses 3*(p^4-p^2+1)/r)."""
+    for v in golden["pairing"]:
+        p = [int(x, 16) for x in v["p"]]
+        q = [int(x, 16) for x in v["q"]]
+        words = engine.test_pairing(sum((limbs(x) for x in p), []), sum((limbs(x) for x in q), []))
+        e = [(int(c[0], 16), int(c[1], 16)) for c in v["e"]]
+        e3 = O.f12_mul(O.f12_mul(e, e), e)
+        tower = [e3[0], e3[2], e3[4], e3[1], e3[3], e3[5]]
+        got = [(from_limbs(words[24 * k:24 * k + 12]), from_limbs(words[24 * k + 12:24 * k + 24])) for k in range(6)]
+        assert got == tower
+
+
+# ------------------------------------------------------------------ the reference KAT through the boundary
+def test_kat_sign_and_verify(engine, golden):
+    kat = golden["kat"]
+    sk = int(kat["sk"], 16).to_bytes(32, "big")
+    msg = bytes.fromhex(kat["msg"])
+    sig = bytes.fromhex(kat["sig"])
+    assert engine.sign(sk, [msg])[0] == sig  # key/curve_test.go:26-29
+    res = engine.verify_messages([msg], [sig], pk48=bytes.fromhex(kat["pk"]))
+    assert res.ok == [True] and res.first_bad is None
+    # negative: wrong message
+    res = engine.verify_messages([msg + b"!"], [sig], pk48=bytes.fromhex(kat["pk"]))
+    assert res.ok == [False] and res.reject_class == [O.REJ_PAIRING] and res.first_bad == 0
+
+
+# ------------------------------------------------------------------ chain.VerifyBeacon / V2
+def test_verify_chained_golden(engine, golden):
+    ch = golden["chained"]
+    engine.set_public_key(bytes.fromhex(ch["pk"]))
+    sigs = [bytes.fromhex(b["sig"]) for b in ch["beacons"]]
+    res = engine.verify_chained(1, bytes.fromhex(ch["genesis_seed"]), sigs)
+    assert all(res.ok) and res.first_bad is None
+    # sub-range starting mid-chain with a 96-byte prev (the client walk from a point of trust)
+    res = engine.verify_chained(5, sigs[3], sigs[4:])
+    assert all(res.ok)
+    # corrupt round 7's signature: rounds 7 and 8 reject (8's message hashes the bad bytes)
+    bad = list(sigs)
+    bad[6] = sigs[5]
+    res = engine.verify_chained(1, bytes.fromhex(ch["genesis_seed"]), bad)
+    assert [i for i, ok in enumerate(res.ok) if not ok] == [6, 7]
+    assert res.first_bad == 7
+
+
+def test_verify_unchained_golden(engine, golden):
+    ch = golden["chained"]
+    engine.set_public_key(bytes.fromhex(ch["pk"]))
+    sigs = [bytes.fromhex(b["sig_v2"]) for b in ch["beacons"]]
+    res = engine.verify_unchained(sigs, first_round=1)
+    assert all(res.ok)
+    rounds = [b["round"] for b in ch["beacons"]]
+    res = engine.verify_unchained(sigs, rounds=rounds)
+    assert all(res.ok)
+    res = engine.verify_unchained(sigs[1:] + sigs[:1], first_round=1)  # wrong rounds
+    assert not any(res.ok) and res.first_bad == 1
+
+
+def test_mixed_batch_golden(engine, golden):
+    mx = golden["mixed"]
+    engine.set_public_key(bytes.fromhex(mx["pk"]))
+    sigs = [bytes.fromhex(s) for s in mx["sigs"]]
+    res = engine.verify_chained(1, bytes.fromhex(mx["genesis_seed"]), sigs)
+    assert res.reject_class == mx["expect_class"]
+    expect_ok = [c == 0 for c in mx["expect_class"]]
+    assert res.ok == expect_ok
+    first = next(i for i, ok in enumerate(expect_ok) if not ok)
+    assert res.first_bad == first + 1
+
+
+# ------------------------------------------------------------------ tbls
+def test_threshold_partials_and_recover(engine, golden):
+    th = golden["threshold"]
+    commits = [bytes.fromhex(c) for c in th["commits"]]
+    engine.set_group(commits, th["n"])
+    msg = bytes.fromhex(th["msg"])
+    partials = [bytes.fromhex(p) for p in th["partials"]]
+    ok, cls = engine.verify_partials(msg, partials)
+    assert all(ok)
+    ok, cls = engine.verify_partials(msg, [bytes.fromhex(th["bad_partial"])])
+    assert ok == [False] and cls == [O.REJ_PAIRING]
+    sub = [bytes.fromhex(p) for p in th["recover_subset"]]
+    sig = engine.recover(msg, sub, th["t"], th["n"])
+    assert sig.hex() == th["group_sig"]
+    # the group signature verifies under commits[0] (VerifyRecovered, chain/beacon/chain.go:141)
+    res = engine.verify_messages([msg], [sig])
+    assert res.ok == [True]
