@@ -44,8 +44,19 @@ struct DBuf {
 
 }  // namespace
 
+// Stage timing (blsv_profile_*): HIP events recorded around every stage launch on the launch stream.
+enum Stage { ST_HASH = 0, ST_DECOMP = 1, ST_MILLER = 2, ST_FEXP = 3, ST_FINISH = 4, ST_N = 5 };
+struct ProfRec {
+  int stage;
+  size_t items;
+  hipEvent_t a, b;
+};
+
 struct blsv_ctx {
   int device = 0;
+  bool prof = false;
+  std::vector<ProfRec> recs;
+  std::vector<hipEvent_t> event_pool;
   hipStream_t stream = nullptr;
   std::string err;
   // group
@@ -94,6 +105,36 @@ static int ensure_workspace(blsv_ctx* c, size_t cnt) {
   return BLSV_OK;
 }
 
+static hipEvent_t take_event(blsv_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Brackets one stage launch with events when profiling is on (no cost otherwise).
+struct StageTimer {
+  blsv_ctx* c;
+  int stage;
+  size_t items;
+  hipStream_t st;
+  hipEvent_t a = nullptr;
+  StageTimer(blsv_ctx* c_, int stage_, size_t items_, hipStream_t st_) : c(c_), stage(stage_), items(items_), st(st_) {
+    if (c->prof && (a = take_event(c))) (void)hipEventRecord(a, st);
+  }
+  ~StageTimer() {
+    if (!a) return;
+    hipEvent_t b = take_event(c);
+    if (!b) return;
+    (void)hipEventRecord(b, st);
+    c->recs.push_back({stage, items, a, b});
+  }
+};
+
 // reduce a 32-byte big-endian scalar mod r -> 8 little-endian words
 static void scalar_mod_r(const uint8_t* be32, uint32_t out[8]) {
   static const uint32_t R[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
@@ -131,12 +172,24 @@ struct PkSel {
 static int run_tail(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t offset, size_t base, size_t cnt,
                     const PkSel& pk, uint64_t* d_bitmap, unsigned long long* d_first_bad, uint8_t* d_cls_out,
                     hipStream_t st) {
-  blsk::launch_decompress_g2(d_sigs, stride, offset, base, cnt, c->S.as<uint32_t>(), c->s_inf.as<uint8_t>(),
-                             c->cls.as<uint8_t>(), st);
-  blsk::launch_miller(pk.tab, pk.inf, pk.idx, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->S.as<uint32_t>(),
-                      c->s_inf.as<uint8_t>(), c->cls.as<uint8_t>(), cnt, c->F.as<uint32_t>(), st);
-  blsk::launch_final_exp(c->F.as<uint32_t>(), cnt, c->cls.as<uint8_t>(), st);
-  blsk::launch_finish(c->cls.as<uint8_t>(), base, cnt, d_bitmap, d_first_bad, st);
+  {
+    StageTimer tm(c, ST_DECOMP, cnt, st);
+    blsk::launch_decompress_g2(d_sigs, stride, offset, base, cnt, c->S.as<uint32_t>(), c->s_inf.as<uint8_t>(),
+                               c->cls.as<uint8_t>(), st);
+  }
+  {
+    StageTimer tm(c, ST_MILLER, cnt, st);
+    blsk::launch_miller(pk.tab, pk.inf, pk.idx, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->S.as<uint32_t>(),
+                        c->s_inf.as<uint8_t>(), c->cls.as<uint8_t>(), cnt, c->F.as<uint32_t>(), st);
+  }
+  {
+    StageTimer tm(c, ST_FEXP, cnt, st);
+    blsk::launch_final_exp(c->F.as<uint32_t>(), cnt, c->cls.as<uint8_t>(), st);
+  }
+  {
+    StageTimer tm(c, ST_FINISH, cnt, st);
+    blsk::launch_finish(c->cls.as<uint8_t>(), base, cnt, d_bitmap, d_first_bad, st);
+  }
   if (d_cls_out) HIPCHK(c, hipMemcpyAsync(d_cls_out + base, c->cls.p, cnt, hipMemcpyDeviceToDevice, st));
   HIPCHK(c, hipGetLastError());
   return BLSV_OK;
@@ -163,7 +216,10 @@ static int verify_driver(blsv_ctx* c, size_t n, const uint8_t* d_sigs, size_t st
   if (rc) return rc;
   for (size_t base = 0; base < n; base += c->cap) {
     const size_t cnt = std::min(c->cap, n - base);
-    hash(base, cnt);
+    {
+      StageTimer tm(c, ST_HASH, cnt, c->stream);
+      hash(base, cnt);
+    }
     rc = run_tail(c, d_sigs, stride, offset, base, cnt, pk, c->bitmap.as<uint64_t>(),
                   c->first_bad.as<unsigned long long>(), reject_class ? c->misc.as<uint8_t>() : nullptr, c->stream);
     if (rc) return rc;
@@ -239,6 +295,12 @@ void blsv_destroy(blsv_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     (void)hipStreamDestroy(c->stream);
   }
+  (void)hipDeviceSynchronize();
+  for (auto& r : c->recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (auto e : c->event_pool) (void)hipEventDestroy(e);
   delete c;
 }
 
@@ -505,7 +567,10 @@ int blsv_verify_chained_dev(blsv_ctx* c, uint64_t first_round, uint64_t seg_len,
                        (uint32_t)seed0_len};
   for (size_t base = 0; base < n; base += c->cap) {
     const size_t cnt = std::min(c->cap, n - base);
-    blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), st);
+    {
+      StageTimer tm(c, ST_HASH, cnt, st);
+      blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), st);
+    }
     rc = run_tail(c, d_sigs96, 96, 0, base, cnt, group_pk(c), d_bitmap, (unsigned long long*)d_first_bad,
                   d_reject_class, st);
     if (rc) return rc;
@@ -530,6 +595,37 @@ int blsv_generate_chained_dev(blsv_ctx* c, const uint8_t* sk32, uint64_t first_r
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(st));  // sk staging buffer is reused by later calls
   return BLSV_OK;
+}
+
+// ------------------------------------------------------------------ stage profiling
+int blsv_profile_enable(blsv_ctx* c, int on) {
+  if (!c) return BLSV_EINVAL;
+  c->prof = on != 0;
+  return BLSV_OK;
+}
+
+int blsv_profile_read(blsv_ctx* c, double* ms, uint64_t* launches, uint64_t* items, int nstages) {
+  if (!c || nstages < 0) return BLSV_EINVAL;
+  (void)hipSetDevice(c->device);
+  for (int s = 0; s < nstages; s++) {
+    if (ms) ms[s] = 0;
+    if (launches) launches[s] = 0;
+    if (items) items[s] = 0;
+  }
+  for (auto& r : c->recs) {
+    HIPCHK(c, hipEventSynchronize(r.b));
+    float t = 0;
+    HIPCHK(c, hipEventElapsedTime(&t, r.a, r.b));
+    if (r.stage < nstages) {
+      if (ms) ms[r.stage] += t;
+      if (launches) launches[r.stage] += 1;
+      if (items) items[r.stage] += r.items;
+    }
+    c->event_pool.push_back(r.a);
+    c->event_pool.push_back(r.b);
+  }
+  c->recs.clear();
+  return ST_N;
 }
 
 // ------------------------------------------------------------------ testing hooks

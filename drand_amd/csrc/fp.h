@@ -10,11 +10,26 @@
 // top limb of p (0x1a0111ea) is < 2^31 - 1 (so t never needs a 13th word). Each limb product is
 // one v_mad_u64_u32 (measured half-rate on gfx950: tools/intrate.hip -> profiles/).
 #pragma once
-#include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "bls_constants.h"
 
+#ifdef BLS_HOST
+// Host build of the device arithmetic (tools/opcount.cpp): the SAME source compiled by clang++ for
+// the CPU, used to count Montgomery multiplications per stage and to run the engine's algorithms
+// on the CPU against the oracle. Never linked into the product library.
+#include <stddef.h>
+#define DI inline
+#define NOINL static inline
+namespace bls {
+extern unsigned long long g_fp_mul_count;
+}
+#define BLS_COUNT_MUL() (++::bls::g_fp_mul_count)
+#else
+#include <hip/hip_runtime.h>
 #define DI __device__ __forceinline__
+#define NOINL static __device__ __noinline__
+#define BLS_COUNT_MUL() ((void)0)
+#endif
 
 namespace bls {
 
@@ -116,7 +131,8 @@ DI fp fp_neg(const fp& a) {
 // body stays within the caller-saved VGPRs so a call costs only the argument moves.
 typedef uint32_t u12 __attribute__((ext_vector_type(12)));
 
-static __device__ __noinline__ u12 fp_mul_u12(u12 a, u12 b) {
+NOINL u12 fp_mul_u12(u12 a, u12 b) {
+  BLS_COUNT_MUL();
   uint32_t t[12];
 #pragma unroll
   for (int j = 0; j < 12; j++) t[j] = 0;
@@ -203,9 +219,9 @@ DI fp fp_pow_words(const fp& a, const uint32_t (&e)[NW]) {
   return r;
 }
 
-static __device__ __noinline__ u12 fp_pow_p_minus_2(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_2)); }
-static __device__ __noinline__ u12 fp_pow_sqrt(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_PLUS_1_DIV_4)); }
-static __device__ __noinline__ u12 fp_pow_legendre(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_1_DIV_2)); }
+NOINL u12 fp_pow_p_minus_2(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_2)); }
+NOINL u12 fp_pow_sqrt(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_PLUS_1_DIV_4)); }
+NOINL u12 fp_pow_legendre(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_1_DIV_2)); }
 
 DI fp fp_inv(const fp& a) { return fp_from_u12(fp_pow_p_minus_2(fp_to_u12(a))); }  // 0 -> 0
 

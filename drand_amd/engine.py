@@ -177,6 +177,23 @@ class Engine:
         self._check(self.lib.blsv_generate_chained_dev(self._h, _lib.buf(sk32), first_round, seg_len, d_seeds,
                                                        seed0_len, d_sigs, n, stream))
 
+    # ------------------------------------------------------------------ stage profiling
+    STAGES = ("hash", "decompress", "miller", "final_exp", "finish")
+
+    def profile(self, on=True):
+        self._check(self.lib.blsv_profile_enable(self._h, 1 if on else 0))
+
+    def profile_read(self):
+        """{stage: (summed ms, launches, items)} since the last read (HIP events on the launch stream)."""
+        n = len(self.STAGES)
+        ms = (ctypes.c_double * n)()
+        la = (ctypes.c_uint64 * n)()
+        it = (ctypes.c_uint64 * n)()
+        rc = self.lib.blsv_profile_read(self._h, ms, la, it, n)
+        if rc < 0:
+            raise EngineError(rc, self.lib.blsv_last_error(self._h).decode())
+        return {s: (ms[k], la[k], it[k]) for k, s in enumerate(self.STAGES)}
+
     # ------------------------------------------------------------------ testing hooks
     def test_fp_mul(self, a_limbs, b_limbs):
         n = len(a_limbs) // 12

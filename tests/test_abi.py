@@ -1,0 +1,78 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads and exports every symbol declared in
+include/*.h, the Python binding declares exactly those symbols, and the host build of the engine's
+own device algorithms (tools/opcount, -DBLS_HOST) verifies golden beacons and reproduces the frozen
+op counts in profiles/opcount.json. No GPU calls."""
+import ctypes
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+from drand_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    syms = set()
+    for h in ("blsverify.h", "blsverify_testing.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        syms |= set(re.findall(r"\b(blsv_\w+)\s*\(", txt))
+    return syms
+
+
+def test_binding_matches_headers():
+    assert header_symbols() == set(_lib.SIGNATURES), header_symbols() ^ set(_lib.SIGNATURES)
+
+
+def test_library_exports_every_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libblsverify.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for s in header_symbols():
+        assert hasattr(lib, s), s
+    lib.blsv_version.restype = ctypes.c_char_p
+    assert b"gfx950" in lib.blsv_version()
+
+
+def test_engine_refuses_without_library(monkeypatch, tmp_path):
+    """No CPU fallback: a missing library is a loud error."""
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.EngineUnavailable):
+        _lib.load()
+
+
+@pytest.fixture(scope="module")
+def opcount_bin():
+    subprocess.run(["make", "-C", os.path.join(ROOT, "tools"), "opcount"], check=True, capture_output=True)
+    return os.path.join(ROOT, "tools", "opcount")
+
+
+def run_opcount(binp, pk, rnd, prev, sig):
+    r = subprocess.run([binp, pk, str(rnd), prev, sig], capture_output=True, text=True)
+    return r.returncode, json.loads(r.stdout)
+
+
+def test_host_build_verifies_golden(opcount_bin, golden):
+    ch = golden["chained"]
+    for b in ch["beacons"][:4]:
+        rc, out = run_opcount(opcount_bin, ch["pk"], b["round"], b["prev"], b["sig"])
+        assert rc == 0 and out["verified"], out
+    frozen = json.load(open(os.path.join(ROOT, "profiles", "opcount.json")))
+    assert out["fp_mul"] == frozen["fp_mul"], "profiles/opcount.json is stale: regenerate it"
+    b = ch["beacons"][2]  # wrong round -> pairing reject
+    rc, out = run_opcount(opcount_bin, ch["pk"], b["round"] + 1, b["prev"], b["sig"])
+    assert rc == 1 and not out["verified"]
+
+
+def test_host_build_decode_classes(opcount_bin, golden):
+    mx = golden["mixed"]
+    for i, c in enumerate(mx["expect_class"]):
+        if c in (2, 3, 4, 5, 6):
+            prev = mx["genesis_seed"] if i == 0 else mx["sigs"][i - 1]
+            rc, out = run_opcount(opcount_bin, mx["pk"], i + 1, prev, mx["sigs"][i])
+            assert out.get("class") == c, (i, out)

@@ -1,0 +1,78 @@
+// Op counter + CPU run of the engine's own device algorithms (drand_amd/csrc/*.h compiled for the host
+// with -DBLS_HOST). Counts Montgomery multiplications (fp_mul_u12 calls; 288 32x32->64 limb products
+// each: 144 for a*b + 144 for m*p in CIOS) per pipeline stage for ONE chained beacon, and checks that
+// the beacon verifies. The counts are the algorithmic work figures used for bench.py's roofline
+// (DESIGN.md §Roofline). Build + run: make -C tools opcount && tools/opcount <pk48hex> <round> <prevhex> <sighex>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../drand_amd/csrc/pairing.h"
+#include "../drand_amd/csrc/hash.h"
+
+namespace bls {
+unsigned long long g_fp_mul_count = 0;
+}
+using namespace bls;
+
+static std::vector<uint8_t> unhex(const char* s) {
+  std::vector<uint8_t> v;
+  size_t n = strlen(s);
+  for (size_t i = 0; i + 1 < n; i += 2) {
+    unsigned x;
+    sscanf(s + i, "%2x", &x);
+    v.push_back((uint8_t)x);
+  }
+  return v;
+}
+
+int main(int argc, char** argv) {
+  if (argc != 5) {
+    fprintf(stderr, "usage: %s pk48hex round prevhex sig96hex\n", argv[0]);
+    return 2;
+  }
+  auto pk = unhex(argv[1]);
+  unsigned long long round = strtoull(argv[2], nullptr, 10);
+  auto prev = unhex(argv[3]);
+  auto sig = unhex(argv[4]);
+  unsigned long long c0;
+
+  // group setup (once per chain, not per beacon)
+  g1a P;
+  bool pinf;
+  if (g1_decompress(pk.data(), P, pinf) != REJ_OK) return 3;
+
+  c0 = g_fp_mul_count;
+  uint32_t msg[8];
+  drand_message(msg, prev.data(), (int)prev.size(), round);
+  g2j h = hash_to_g2(msg);
+  g2a ha = g2_to_aff(h);
+  unsigned long long n_hash = g_fp_mul_count - c0;
+
+  c0 = g_fp_mul_count;
+  g2a s;
+  bool sinf;
+  uint8_t cls = g2_decompress(sig.data(), s, sinf, true);
+  unsigned long long n_decomp = g_fp_mul_count - c0;
+  if (cls) {
+    printf("{\"verified\": false, \"class\": %d}\n", cls);
+    return 1;
+  }
+
+  c0 = g_fp_mul_count;
+  g1a Ps[2] = {P, {fp_load_const(G1_GEN_X), fp_load_const(G1_GEN_NEG_Y)}};
+  g2a Qs[2] = {ha, s};
+  bool act[2] = {true, true};
+  fp12 f = miller_loop_multi<2>(Ps, Qs, act);
+  unsigned long long n_miller = g_fp_mul_count - c0;
+
+  c0 = g_fp_mul_count;
+  bool ok = fp12_is_one(final_exponentiation(f));
+  unsigned long long n_fexp = g_fp_mul_count - c0;
+
+  printf("{\"verified\": %s, \"fp_mul\": {\"hash\": %llu, \"decompress\": %llu, \"miller\": %llu, \"final_exp\": %llu},"
+         " \"limb_products_per_fp_mul\": 288}\n",
+         ok ? "true" : "false", n_hash, n_decomp, n_miller, n_fexp);
+  return ok ? 0 : 1;
+}
