@@ -69,7 +69,7 @@ struct blsv_ctx {
   bool pk_cache_valid = false;
   // staging workspace
   size_t cap = 0;
-  DBuf H, S, F, h_inf, s_inf, cls;
+  DBuf H, S, F, FW, h_inf, s_inf, cls;
   // inputs / outputs
   DBuf in_sigs, in_msgs, in_off, in_len, in_rounds, seeds, bitmap, first_bad, sk, idx, lambdas, scratch, out,
       pp_tab, pp_inf, sel, g1_cls, misc;
@@ -98,6 +98,7 @@ static int ensure_workspace(blsv_ctx* c, size_t cnt) {
   HIPCHK(c, c->H.ensure(want * blsk::H_WORDS * 4));
   HIPCHK(c, c->S.ensure(want * blsk::S_WORDS * 4));
   HIPCHK(c, c->F.ensure(want * blsk::F_WORDS * 4));
+  HIPCHK(c, c->FW.ensure(3 * want * blsk::F_WORDS * 4));
   HIPCHK(c, c->h_inf.ensure(want));
   HIPCHK(c, c->s_inf.ensure(want));
   HIPCHK(c, c->cls.ensure(want));
@@ -184,7 +185,7 @@ static int run_tail(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t of
   }
   {
     StageTimer tm(c, ST_FEXP, cnt, st);
-    blsk::launch_final_exp(c->F.as<uint32_t>(), cnt, c->cls.as<uint8_t>(), st);
+    blsk::launch_final_exp(c->F.as<uint32_t>(), c->FW.as<uint32_t>(), cnt, c->cls.as<uint8_t>(), st);
   }
   {
     StageTimer tm(c, ST_FINISH, cnt, st);

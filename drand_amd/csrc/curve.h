@@ -298,7 +298,7 @@ DI uint8_t g1_decompress(const uint8_t* in, g1a& out, bool& is_inf) {
   if (!fp_raw_lt_p(xr)) return REJ_X_GE_P;
   fp x = fp_to_mont(xr);
   fp rhs = fp_add(fp_mul(fp_sqr(x), x), fp_mul4(fp_one()));
-  fp y = fp_sqrt_cand(rhs);
+  fp y = fp_mul(fp_pow_sqrt_inv(rhs), rhs);
   if (!fp_eq(fp_sqr(y), rhs)) return REJ_NOT_ON_CURVE;
   if (fp_raw_gt_half(fp_from_mont(y)) != sign) y = fp_neg(y);
   out.x = x;

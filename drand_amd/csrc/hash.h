@@ -218,25 +218,31 @@ DI void hash_to_field_fp2(const uint32_t (&msg)[8], fp2& u0, fp2& u1) {
 DI g2j hash_field_to_g2(const fp2& u0, const fp2& u1);
 
 // RFC 9380 §6.6.2 simplified SWU onto E2': y^2 = x^3 + A'x + B' (straight-line form, selects
-// instead of branches so a wave never diverges on the is_square outcome)
-DI g2a map_to_curve_sswu(const fp2& u) {
+// instead of branches so a wave never diverges on the is_square outcome).
+//   tv1 = 1/(Z^2 u^4 + Z u^2) is supplied by the caller (both u of a hash share one inversion).
+//   Square test and root of the norm come from ONE Fp exponentiation: gx2 = (Z u^2)^3 gx1, so
+//   when N(gx1) is a non-residue, sqrt(N(gx2)) = N(u)^3 sqrt(-N(Z)^3) sqrt(-N(gx1)).
+DI fp2 sswu_den(const fp2& u) {
+  fp2 zu2 = fp2_mul(fp2_load_const(SSWU_Z), fp2_sqr(u));
+  return fp2_add(fp2_sqr(zu2), zu2);
+}
+
+DI g2a map_to_curve_sswu(const fp2& u, const fp2& tv1) {
   const fp2 A = fp2_load_const(SSWU_A);
   const fp2 B = fp2_load_const(SSWU_B);
-  const fp2 Z = fp2_load_const(SSWU_Z);
-  fp2 u2 = fp2_sqr(u);
-  fp2 zu2 = fp2_mul(Z, u2);
-  fp2 den = fp2_add(fp2_sqr(zu2), zu2);
-  fp2 tv1 = fp2_inv(den);  // inv0: 0 -> 0
+  fp2 zu2 = fp2_mul(fp2_load_const(SSWU_Z), fp2_sqr(u));
   fp2 x1 = fp2_mul(fp2_load_const(SSWU_MINUS_B_OVER_A), fp2_add(fp2_one(), tv1));
   x1 = fp2_select(fp2_is_zero(tv1), fp2_load_const(SSWU_B_OVER_ZA), x1);
   fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), A), x1), B);
   fp2 x2 = fp2_mul(zu2, x1);
-  fp2 gx2 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x2), A), x2), B);
-  bool sq1 = fp2_is_square(gx1);
+  fp2 gx2 = fp2_mul(fp2_mul(fp2_sqr(zu2), zu2), gx1);
+  bool sq1;
+  fp r1 = fp_norm_root(fp2_norm(gx1), sq1);  // sqrt(N(gx1)) or sqrt(-N(gx1))
+  fp nu = fp2_norm(u);
+  fp r2 = fp_mul(fp_mul(fp_mul(fp_sqr(nu), nu), fp_load_const(SSWU_SQRT_MINUS_NZ3)), r1);
   fp2 x = fp2_select(sq1, x1, x2);
   fp2 gx = fp2_select(sq1, gx1, gx2);
-  fp2 y;
-  fp2_sqrt(y, gx);
+  fp2 y = fp2_sqrt_with_norm_root(gx, fp_select(sq1, r1, r2));
   if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
   return {x, y};
 }
@@ -267,8 +273,16 @@ DI g2j iso_map_g2(const g2a& p) {
 }
 
 DI g2j hash_field_to_g2(const fp2& u0, const fp2& u1) {
-  g2j q0 = iso_map_g2(map_to_curve_sswu(u0));
-  g2j q1 = iso_map_g2(map_to_curve_sswu(u1));
+  // one inversion for both SSWU denominators (exact also when one of them is 0: inv0(0) = 0)
+  fp2 d0 = sswu_den(u0), d1 = sswu_den(u1);
+  const bool z0 = fp2_is_zero(d0), z1 = fp2_is_zero(d1);
+  d0 = fp2_select(z0, fp2_one(), d0);
+  d1 = fp2_select(z1, fp2_one(), d1);
+  fp2 di = fp2_inv(fp2_mul(d0, d1));
+  fp2 tv0 = fp2_select(z0, fp2_zero(), fp2_mul(d1, di));
+  fp2 tv1 = fp2_select(z1, fp2_zero(), fp2_mul(d0, di));
+  g2j q0 = iso_map_g2(map_to_curve_sswu(u0, tv0));
+  g2j q1 = iso_map_g2(map_to_curve_sswu(u1, tv1));
   return g2_clear_cofactor(jac_add(q0, q1));
 }
 

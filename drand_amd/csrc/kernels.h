@@ -43,7 +43,8 @@ void launch_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, siz
 void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
                    const uint8_t* h_inf, const uint32_t* S, const uint8_t* s_inf, const uint8_t* cls, size_t cnt,
                    uint32_t* F, hipStream_t st);
-void launch_final_exp(const uint32_t* F, size_t cnt, uint8_t* cls, hipStream_t st);
+// F is clobbered; W = 3 * cnt * F_WORDS words of staging
+void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st);
 // bitmap bit (base+i) = (cls[i] == 0); bitmap must cover whole 64-bit words; first_bad = min index
 void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap, unsigned long long* first_bad,
                    hipStream_t st);

@@ -22,14 +22,19 @@ struct g2proj {
   fp2 x, y, z;
 };
 
+// 3b' C = 12 (1 + i) C by additions
+DI fp2 fp2_mul_3b(const fp2& c) {
+  fp2 x4 = fp2_dbl(fp2_dbl(fp2_mul_xi(c)));
+  return fp2_add(fp2_dbl(x4), x4);
+}
+
 DI void miller_dbl_step(g2proj& t, fp2& l00, fp2& l01, fp2& l11, const fp& xp, const fp& yp) {
-  const fp inv2 = fp_load_const(FP_INV2);
-  fp2 A = fp2_mul_fp(fp2_mul(t.x, t.y), inv2);
+  fp2 A = fp2_half(fp2_mul(t.x, t.y));
   fp2 B = fp2_sqr(t.y);
   fp2 C = fp2_sqr(t.z);
-  fp2 E = fp2_mul(C, fp2_load_const(B2_TWIST_X3));
+  fp2 E = fp2_mul_3b(C);
   fp2 F = fp2_mul3(E);
-  fp2 G = fp2_mul_fp(fp2_add(B, F), inv2);
+  fp2 G = fp2_half(fp2_add(B, F));
   fp2 H = fp2_sub(fp2_sqr(fp2_add(t.y, t.z)), fp2_add(B, C));
   fp2 X2 = fp2_sqr(t.x);
   l00 = fp2_sub(E, B);
@@ -57,8 +62,72 @@ DI void miller_add_step(g2proj& t, const g2a& q, fp2& l00, fp2& l01, fp2& l11, c
   t.z = fp2_mul(t.z, E);
 }
 
-// f = prod_{k<npairs, active} f_{|x|, Q_k}(P_k), conjugated (x < 0). Inactive pairs (a point at
-// infinity, skipped like kilic's Engine) contribute 1.
+// Sparse line l = l00 + l01 v + l11 v w (tower slots c0.c0, c0.c1, c1.c1).
+struct line {
+  fp2 a0, a1, a4;
+};
+
+// Product of two sparse lines (6 Fp2 mul); c1.c0 of the result is zero:
+//   c0 = (a0 b0 + xi a4 b4, a0 b1 + a1 b0, a1 b1),  c1 = (0, a0 b4 + a4 b0, a1 b4 + a4 b1)
+DI fp12 line_mul_line(const line& a, const line& b) {
+  fp2 t00 = fp2_mul(a.a0, b.a0), t11 = fp2_mul(a.a1, b.a1), t44 = fp2_mul(a.a4, b.a4);
+  fp2 c01 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.a0, a.a1), fp2_add(b.a0, b.a1)), t00), t11);
+  fp2 c11 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.a0, a.a4), fp2_add(b.a0, b.a4)), t00), t44);
+  fp2 c12 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.a1, a.a4), fp2_add(b.a1, b.a4)), t11), t44);
+  return {{fp2_add(t00, fp2_mul_xi(t44)), c01, t11}, {fp2_zero(), c11, c12}};
+}
+
+// a * (b1 v + b2 v^2) (5 Fp2 mul)
+DI fp6 fp6_mul_by_12(const fp6& a, const fp2& b1, const fp2& b2) {
+  fp2 t1 = fp2_mul(a.c1, b1), t2 = fp2_mul(a.c2, b2);
+  fp2 m = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b1, b2)), t1), t2);  // a1 b2 + a2 b1
+  return {fp2_mul_xi(m), fp2_add(fp2_mul(a.c0, b1), fp2_mul_xi(t2)), fp2_add(fp2_mul(a.c0, b2), t1)};
+}
+
+// f * L for L with L.c1.c0 == 0 (the product of two lines): 6 + 5 + 6 Fp2 mul
+DI fp12 fp12_mul_by_line_pair(const fp12& f, const fp12& L) {
+  fp6 t0 = fp6_mul(f.c0, L.c0);
+  fp6 t1 = fp6_mul_by_12(f.c1, L.c1.c1, L.c1.c2);
+  fp6 Ls = {L.c0.c0, fp2_add(L.c0.c1, L.c1.c1), fp2_add(L.c0.c2, L.c1.c2)};
+  fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(f.c0, f.c1), Ls), t0), t1);
+  return {fp6_add(t0, fp6_mul_v(t1)), c1};
+}
+
+DI line line_one() { return {fp2_one(), fp2_zero(), fp2_zero()}; }
+
+// f = prod_k f_{|x|, Q_k}(P_k), conjugated (x < 0), for exactly two pairs: the two lines of a
+// step are multiplied together first and then into f. Inactive pairs (a point at infinity,
+// skipped like kilic's Engine) contribute the line 1.
+DI fp12 miller_loop_2(const g1a (&P)[2], const g2a (&Q)[2], const bool (&active)[2]) {
+  g2proj T[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) T[k] = {Q[k].x, Q[k].y, fp2_one()};
+  fp12 f = fp12_one();
+  bool first = true;
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    if (!first) f = fp12_sqr(f);
+    line l[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      miller_dbl_step(T[k], l[k].a0, l[k].a1, l[k].a4, P[k].x, P[k].y);
+      if (!active[k]) l[k] = line_one();
+    }
+    f = fp12_mul_by_line_pair(f, line_mul_line(l[0], l[1]));
+    first = false;
+    if ((BLS_X_ABS >> i) & 1ull) {
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        miller_add_step(T[k], Q[k], l[k].a0, l[k].a1, l[k].a4, P[k].x, P[k].y);
+        if (!active[k]) l[k] = line_one();
+      }
+      f = fp12_mul_by_line_pair(f, line_mul_line(l[0], l[1]));
+    }
+  }
+  return fp12_conj(f);
+}
+
+// single-pair form (test hook): same lines, f multiplied by each sparse line
 template <int NP>
 DI fp12 miller_loop_multi(const g1a (&P)[NP], const g2a (&Q)[NP], const bool (&active)[NP]) {
   g2proj T[NP];
@@ -88,29 +157,58 @@ DI fp12 miller_loop_multi(const g1a (&P)[NP], const g2a (&Q)[NP], const bool (&a
   return fp12_conj(f);
 }
 
-// g^|x| for g in the cyclotomic subgroup
-DI fp12 fp12_pow_x_abs(const fp12& g) {
-  fp12 r = g;
+// Final exponentiation f^(3 (p^12 - 1)/r), split into stages so that the device can run each as its
+// own kernel with only one or two Fp12 values live (the operands are re-read from HBM staging at
+// each use through the `load` callables instead of being held in registers):
+//   easy : g = f^((p^6 - 1)(p^2 + 1))
+//   hard : 3 (p^4 - p^2 + 1)/r = (x-1)^2 (x+p) (x^2+p^2-1) + 3 with x = -|x|, i.e.
+//     a = g^(x-1)           step<0>(g)
+//     b = a^(x-1)           step<1>(a)
+//     c = b^(x+p)           step<2>(b)
+//     t = c^x               step<3>(c)
+//     e = t^x c^(p^2) c^-1 g^3   step<4>(t; c, g)
+// g^|x| uses Granger-Scott cyclotomic squarings; |x| = 0xd201000000010000 has bits 63,62,60,57,48,16,
+// i.e. runs of 1, 2, 3, 9, 32 squarings each followed by a multiplication, then 16 squarings.
+DI fp12 fexp_easy(const fp12& f) {
+  fp12 t = fp12_mul(fp12_conj(f), fp12_inv(f));  // f^(p^6 - 1)
+  return fp12_mul(fp12_frob2(t), t);             // ^(p^2 + 1)
+}
+
+template <typename Load>
+DI fp12 fp12_pow_x_abs_reload(Load load) {
+  constexpr uint64_t NSQ = 1ull | (2ull << 6) | (3ull << 12) | (9ull << 18) | (32ull << 24) | (16ull << 30);
+  fp12 r = load();
 #pragma unroll 1
-  for (int i = 62; i >= 0; i--) {
-    r = fp12_sqr(r);
-    if ((BLS_X_ABS >> i) & 1ull) r = fp12_mul(r, g);
+  for (int s = 0; s < 6; s++) {
+    const int n = (int)((NSQ >> (6 * s)) & 63u);
+#pragma unroll 1
+    for (int k = 0; k < n; k++) r = fp12_cyclotomic_sqr(r);
+    if (s < 5) r = fp12_mul(r, load());
   }
   return r;
 }
 
-// g^x, x = -|x| (inverse = conjugate in the cyclotomic subgroup)
-DI fp12 fp12_pow_x(const fp12& g) { return fp12_conj(fp12_pow_x_abs(g)); }
+template <int MODE, typename LX, typename LC, typename LG>
+DI fp12 fexp_step(LX lx, LC lc, LG lg) {
+  fp12 r = fp12_conj(fp12_pow_x_abs_reload(lx));  // X^x (inverse = conjugate in the cyclotomic subgroup)
+  if (MODE == 0 || MODE == 1) return fp12_mul(r, fp12_conj(lx()));
+  if (MODE == 2) return fp12_mul(r, fp12_frob(lx()));
+  if (MODE == 3) return r;
+  r = fp12_mul(r, fp12_frob2(lc()));
+  r = fp12_mul(r, fp12_conj(lc()));
+  r = fp12_mul(r, fp12_cyclotomic_sqr(lg()));
+  return fp12_mul(r, lg());
+}
 
-// f^(3 (p^12 - 1) / r)
+// whole final exponentiation in registers (host op counter, test hooks)
 DI fp12 final_exponentiation(const fp12& f) {
-  fp12 t = fp12_mul(fp12_conj(f), fp12_inv(f));  // f^(p^6 - 1)
-  fp12 g = fp12_mul(fp12_frob2(t), t);           // ^(p^2 + 1)
-  fp12 a = fp12_mul(fp12_pow_x(g), fp12_conj(g));        // g^(x-1)
-  fp12 b = fp12_mul(fp12_pow_x(a), fp12_conj(a));        // g^((x-1)^2)
-  fp12 c = fp12_mul(fp12_pow_x(b), fp12_frob(b));        // b^(x+p)
-  fp12 d = fp12_mul(fp12_mul(fp12_pow_x(fp12_pow_x(c)), fp12_frob2(c)), fp12_conj(c));  // c^(x^2+p^2-1)
-  return fp12_mul(d, fp12_mul(fp12_sqr(g), g));  // * g^3
+  const fp12 g = fexp_easy(f);
+  auto none = [&]() { return g; };
+  const fp12 a = fexp_step<0>([&]() { return g; }, none, none);
+  const fp12 b = fexp_step<1>([&]() { return a; }, none, none);
+  const fp12 c = fexp_step<2>([&]() { return b; }, none, none);
+  const fp12 t = fexp_step<3>([&]() { return c; }, none, none);
+  return fexp_step<4>([&]() { return t; }, [&]() { return c; }, [&]() { return g; });
 }
 
 }  // namespace bls

@@ -59,14 +59,24 @@ def run_opcount(binp, pk, rnd, prev, sig):
 
 def test_host_build_verifies_golden(opcount_bin, golden):
     ch = golden["chained"]
-    for b in ch["beacons"][:4]:
+    for b in ch["beacons"]:
         rc, out = run_opcount(opcount_bin, ch["pk"], b["round"], b["prev"], b["sig"])
         assert rc == 0 and out["verified"], out
+        rc2, out2 = run_opcount(opcount_bin, ch["pk"], b["round"], "-", b["sig_v2"])
+        assert rc2 == 0 and out2["verified"], out2
     frozen = json.load(open(os.path.join(ROOT, "profiles", "opcount.json")))
     assert out["fp_mul"] == frozen["fp_mul"], "profiles/opcount.json is stale: regenerate it"
     b = ch["beacons"][2]  # wrong round -> pairing reject
     rc, out = run_opcount(opcount_bin, ch["pk"], b["round"] + 1, b["prev"], b["sig"])
     assert rc == 1 and not out["verified"]
+
+
+def test_host_build_hash_to_g2_golden(opcount_bin, golden):
+    for v in golden["hash_to_g2"]:
+        r = subprocess.run([opcount_bin, "hash", v["msg"]], capture_output=True, text=True, check=True)
+        got = json.loads(r.stdout)
+        assert [int(x, 16) for x in got["x"]] == [int(x, 16) for x in v["x"]]
+        assert [int(x, 16) for x in got["y"]] == [int(x, 16) for x in v["y"]]
 
 
 def test_host_build_decode_classes(opcount_bin, golden):

@@ -27,9 +27,38 @@ static std::vector<uint8_t> unhex(const char* s) {
   return v;
 }
 
+static void print_fp(const fp& a) {
+  fp r = fp_from_mont(a);
+  printf("\"");
+  for (int i = 11; i >= 0; i--) printf("%08x", r.l[i]);
+  printf("\"");
+}
+
+// hash <msghex>: KyberG2.Hash of an arbitrary message (xmd_b0_bytes path), affine raw coordinates
+static int cmd_hash(const char* msghex) {
+  auto msg = unhex(msghex);
+  uint32_t b0[8];
+  xmd_b0_bytes(b0, msg.data(), (uint32_t)msg.size(), DST);
+  fp2 u0, u1;
+  xmd_tail_to_field(b0, u0, u1);
+  g2a h = g2_to_aff(hash_field_to_g2(u0, u1));
+  printf("{\"x\": [");
+  print_fp(h.x.c0);
+  printf(", ");
+  print_fp(h.x.c1);
+  printf("], \"y\": [");
+  print_fp(h.y.c0);
+  printf(", ");
+  print_fp(h.y.c1);
+  printf("]}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc == 3 && !strcmp(argv[1], "hash")) return cmd_hash(argv[2]);
   if (argc != 5) {
-    fprintf(stderr, "usage: %s pk48hex round prevhex sig96hex\n", argv[0]);
+    fprintf(stderr, "usage: %s pk48hex round prevhex|- sig96hex   (prev '-' = unchained V2)\n       %s hash msghex\n",
+            argv[0], argv[0]);
     return 2;
   }
   auto pk = unhex(argv[1]);
@@ -45,7 +74,10 @@ int main(int argc, char** argv) {
 
   c0 = g_fp_mul_count;
   uint32_t msg[8];
-  drand_message(msg, prev.data(), (int)prev.size(), round);
+  if (!strcmp(argv[3], "-"))
+    drand_message_v2(msg, round);
+  else
+    drand_message(msg, prev.data(), (int)prev.size(), round);
   g2j h = hash_to_g2(msg);
   g2a ha = g2_to_aff(h);
   unsigned long long n_hash = g_fp_mul_count - c0;
@@ -64,7 +96,7 @@ int main(int argc, char** argv) {
   g1a Ps[2] = {P, {fp_load_const(G1_GEN_X), fp_load_const(G1_GEN_NEG_Y)}};
   g2a Qs[2] = {ha, s};
   bool act[2] = {true, true};
-  fp12 f = miller_loop_multi<2>(Ps, Qs, act);
+  fp12 f = miller_loop_2(Ps, Qs, act);
   unsigned long long n_miller = g_fp_mul_count - c0;
 
   c0 = g_fp_mul_count;
