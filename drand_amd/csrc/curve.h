@@ -197,16 +197,21 @@ DI bool g2_in_subgroup(const g2j& p) {
 }
 
 // RFC 9380 G.3 clear_cofactor_bls12381_g2: h_eff P = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)
+// regrouped so that only two points are live across each [x] multiplication:
+//   A = [x]P + psi(P),  B = [x]A = [x^2]P + [x]psi(P),  h_eff P = B - A - P + psi^2(2P)
+// `reload` returns P again (the caller may re-read it from memory instead of keeping it live).
+template <typename Reload>
+DI g2j g2_clear_cofactor_reload(Reload reload) {
+  g2j p = reload();
+  g2j a = jac_add(jac_neg(jac_mul_x_abs(p)), g2_psi(p));
+  g2j r = jac_add(jac_neg(jac_mul_x_abs(a)), jac_neg(a));
+  p = reload();
+  r = jac_add(r, jac_neg(p));
+  return jac_add(r, g2_psi2(jac_dbl(p)));
+}
+
 DI g2j g2_clear_cofactor(const g2j& p) {
-  g2j t1 = jac_neg(jac_mul_x_abs(p));  // [x]P
-  g2j t2 = g2_psi(p);
-  g2j t3 = g2_psi2(jac_dbl(p));
-  t3 = jac_add(t3, jac_neg(t2));
-  t2 = jac_add(t1, t2);
-  t2 = jac_neg(jac_mul_x_abs(t2));
-  t3 = jac_add(t3, t2);
-  t3 = jac_add(t3, jac_neg(t1));
-  return jac_add(t3, jac_neg(p));
+  return g2_clear_cofactor_reload([&]() { return p; });
 }
 
 // ------------------------------------------------------------ G1 subgroup check

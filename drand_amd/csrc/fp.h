@@ -1,14 +1,13 @@
 // Fp arithmetic for BLS12-381 on gfx950: 381-bit prime field, 12 x 32-bit little-endian limbs,
-// Montgomery form (R = 2^384), values kept canonical in [0, p).
+// Montgomery form (R = 2^392, see fp_mul_u12), values kept canonical in [0, p).
 //
 // This is the engine's replacement for kilic/bls12-381's fp.go + the amd64 assembly Montgomery
 // multiply (the [ext] native code on the reference path). Everything above this
 // file (fp2/fp6/fp12, curves, hash-to-curve, pairing) only uses the fp_* API below, so the limb
 // representation can change without touching the tower.
 //
-// Multiplication: CIOS Montgomery with the "no final carry word" simplification, valid because the
-// top limb of p (0x1a0111ea) is < 2^31 - 1 (so t never needs a 13th word). Each limb product is
-// one v_mad_u64_u32 (measured half-rate on gfx950: tools/intrate.hip -> profiles/).
+// Multiplication: Montgomery product scanning in radix 2^28 (fp_mul_u12 below); each limb product
+// is one v_mad_u64_u32 (full rate on gfx950: tools/intrate.hip -> profiles/intrate.json).
 #pragma once
 #include <stdint.h>
 #include "bls_constants.h"
@@ -140,94 +139,80 @@ DI fp fp_neg(const fp& a) {
 
 typedef uint32_t u12 __attribute__((ext_vector_type(12)));
 
-// Montgomery product a*b*R^-1 mod p.
+// Montgomery product a*b*R^-1 mod p, R = 2^392.
 // Deliberately NOT inlined: one copy of the body per code object keeps kernels small
 // (instruction-cache resident) and compile times sane. Arguments/results are ext_vector u12 so
-// they travel in v0..v23 / v0..v11 (a by-value struct would be passed through scratch), and the
-// body stays within the caller-saved VGPRs so a call costs only the argument moves.
+// they travel in v0..v23 / v0..v11 (a by-value struct would be passed through scratch).
 //
-// Device: FIPS (finely integrated product scanning). Column k of a*b and of m*p accumulates into a
-// 96-bit (acc64, top) register triple: each limb product is ONE v_mad_u64_u32 (64-bit addend = the
-// accumulator itself, carry-out -> VCC) + ONE v_addc_co_u32 folding the carry into `top`, so there
-// are no per-product moves (the compiler's CIOS needs ~2.2 moves + a 64-bit add per product:
-// tools/fpbench.hip measured 43.4 G (CIOS) vs 59.3 G (this) fp_mul/s on one MI355X).
-// Column sums stay < 2^69 (24 products < 2^64 each + the carried column), and the result of the
-// last column is < 2p < 2^382, so 12 output limbs + one conditional subtraction suffice.
-#ifndef BLS_HOST
-#define BLS_MAC2(acc, top, x, y, mm, ps)                                                      \
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc\n\t"   \
-      "v_mad_u64_u32 %0, vcc, %4, %5, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"         \
-      : "+v"(acc), "+v"(top)                                                                 \
-      : "v"(x), "v"(y), "v"(mm), "s"(ps)                                                     \
-      : "vcc")
-#define BLS_MAC(acc, top, x, y)                                                               \
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"         \
-      : "+v"(acc), "+v"(top)                                                                 \
-      : "v"(x), "v"(y)                                                                       \
-      : "vcc")
-#define BLS_MACS(acc, top, x, ys)                                                             \
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"         \
-      : "+v"(acc), "+v"(top)                                                                 \
-      : "v"(x), "s"(ys)                                                                      \
-      : "vcc")
+// Storage stays 12 x 32-bit limbs; the product runs in radix 2^28 (14 limbs): every limb product is
+// < 2^56, so a whole column (<= 28 products + the carried-in column < 2^62) accumulates in one
+// 64-bit register with plain v_mad_u64_u32 -- no carry-propagation instructions at all (the
+// 32-bit-limb form needs one v_addc per product): 588 VALU instructions per multiply instead of
+// ~825, measured 67.7 G vs 59.8 G fp_mul/s on one MI355X (tools/fpbench.hip, profiles/).
+// Product scanning with interleaved reduction (FIPS): column k adds a_j b_{k-j} + m_j p_{k-j};
+// m_k = (low 28 bits of the column) * (-p^-1) mod 2^28. With inputs < p the result is < 2p (4p < R),
+// so one conditional subtraction in the 32-bit form restores [0, p).
+// Constants (bls_constants.h) are generated for R = 2^392 (gen_constants.py).
+constexpr uint32_t M28 = (1u << 28) - 1u;
+
+DI void fp_split28(const u12& a, uint32_t (&x)[14]) {
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    const int w = (28 * k) >> 5, s = (28 * k) & 31;
+    const uint64_t cat = ((uint64_t)(w + 1 < 12 ? a[w + 1] : 0u) << 32) | a[w];
+    x[k] = (uint32_t)(cat >> s) & M28;
+  }
+}
+
+// 14 x 28-bit limbs (top limb < 2^18, value < 2p) -> canonical 12 x 32-bit
+DI u12 fp_join28_reduce(const uint32_t (&t)[14]) {
+  uint32_t r32[12];
+#pragma unroll
+  for (int w = 0; w < 12; w++) {
+    const int k = (32 * w) / 28, s = (32 * w) % 28;  // s <= 24: two limbs cover the word
+    r32[w] = (t[k] >> s) | (t[k + 1] << (28 - s));
+  }
+  uint32_t d[12];
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(r32[i], P_RAW[i], br, &br);
+  u12 r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r[i] = br ? r32[i] : d[i];
+  return r;
+}
 
 NOINL u12 fp_mul_u12(u12 a, u12 b) {
-  uint32_t m[12], t[12];
-  uint64_t acc = 0;
-  uint32_t top = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-#pragma unroll
-    for (int j = 0; j < i; j++) BLS_MAC2(acc, top, a[j], b[i - j], m[j], P_RAW[i - j]);
-    BLS_MAC(acc, top, a[i], b[0]);
-    m[i] = (uint32_t)acc * P_INV32;
-    BLS_MACS(acc, top, m[i], P_RAW[0]);  // low word becomes 0
-    acc = (acc >> 32) | ((uint64_t)top << 32);
-    top = 0;
-  }
-#pragma unroll
-  for (int i = 12; i < 24; i++) {
-#pragma unroll
-    for (int j = i - 11; j < 12; j++) BLS_MAC2(acc, top, a[j], b[i - j], m[j], P_RAW[i - j]);
-    t[i - 12] = (uint32_t)acc;
-    acc = (acc >> 32) | ((uint64_t)top << 32);
-    top = 0;
-  }
-  uint32_t d[12];
-  unsigned br = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(t[i], P_RAW[i], br, &br);
-  u12 r;
-#pragma unroll
-  for (int i = 0; i < 12; i++) r[i] = br ? t[i] : d[i];
-  return r;
-}
-#else
-// Host (tools/opcount): portable CIOS, same results.
-NOINL u12 fp_mul_u12(u12 a, u12 b) {
   BLS_COUNT_MUL();
-  uint32_t t[12];
-  for (int j = 0; j < 12; j++) t[j] = 0;
-  for (int i = 0; i < 12; i++) {
-    const uint32_t bi = b[i];
-    uint64_t A = (uint64_t)a[0] * bi + t[0];
-    const uint32_t m = (uint32_t)A * P_INV32;
-    uint64_t C = (uint64_t)m * P_RAW[0] + (uint32_t)A;
-    for (int j = 1; j < 12; j++) {
-      A = (uint64_t)a[j] * bi + t[j] + (A >> 32);
-      C = (uint64_t)m * P_RAW[j] + (uint32_t)A + (C >> 32);
-      t[j - 1] = (uint32_t)C;
+  uint32_t x[14], y[14], m[14], t[14];
+  fp_split28(a, x);
+  fp_split28(b, y);
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+#pragma unroll
+    for (int j = 0; j < k; j++) {
+      acc += (uint64_t)x[j] * y[k - j];
+      acc += (uint64_t)m[j] * P28[k - j];
     }
-    t[11] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+    acc += (uint64_t)x[k] * y[0];
+    m[k] = ((uint32_t)acc * P_INV28) & M28;
+    acc += (uint64_t)m[k] * P28[0];  // low 28 bits become 0
+    acc >>= 28;
   }
-  uint32_t d[12];
-  unsigned br = 0;
-  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(t[i], P_RAW[i], br, &br);
-  u12 r;
-  for (int i = 0; i < 12; i++) r[i] = br ? t[i] : d[i];
-  return r;
+#pragma unroll
+  for (int k = 14; k < 27; k++) {
+#pragma unroll
+    for (int j = k - 13; j < 14; j++) {
+      acc += (uint64_t)x[j] * y[k - j];
+      acc += (uint64_t)m[j] * P28[k - j];
+    }
+    t[k - 14] = (uint32_t)acc & M28;
+    acc >>= 28;
+  }
+  t[13] = (uint32_t)acc;  // < 2^18: the result is < 2p < 2^382
+  return fp_join28_reduce(t);
 }
-#endif
 
 DI u12 fp_to_u12(const fp& a) {
   u12 v;

@@ -125,12 +125,13 @@ DI fp fp_from_be512(const uint32_t* w) {
   return fp_add(fp_mul(hi, fp_load_const(FP_2POW256_R2)), fp_mul(lo, fp_load_const(FP_R2)));
 }
 
-// b_1..b_8 of expand_message_xmd from b_0, then the four 64-byte field elements
+// b_1..b_8 of expand_message_xmd from b_0, then the four 64-byte field elements; each element is
+// reduced as soon as its two blocks exist (16 words live instead of 64)
 DI void xmd_tail_to_field(const uint32_t (&b0)[8], fp2& u0, fp2& u1) {
-  uint32_t uni[64];  // b1..b8
   uint32_t prev[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) prev[i] = 0;
+  fp e[4];
 #pragma unroll
   for (int k = 1; k <= 8; k++) {
     uint32_t st[8];
@@ -144,16 +145,22 @@ DI void xmd_tail_to_field(const uint32_t (&b0)[8], fp2& u0, fp2& u1) {
     blk[8] |= (uint32_t)k << 24;
     sha256_compress(st, blk);
     sha256_compress(st, XMD_BI_B);
+    if (k & 1) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      prev[i] = st[i];
-      uni[(k - 1) * 8 + i] = st[i];
+      for (int i = 0; i < 8; i++) prev[i] = st[i];
+    } else {
+      uint32_t w[16];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        w[i] = prev[i];
+        w[8 + i] = st[i];
+        prev[i] = st[i];
+      }
+      e[k / 2 - 1] = fp_from_be512(w);
     }
   }
-  u0.c0 = fp_from_be512(uni + 0);
-  u0.c1 = fp_from_be512(uni + 16);
-  u1.c0 = fp_from_be512(uni + 32);
-  u1.c1 = fp_from_be512(uni + 48);
+  u0 = {e[0], e[1]};
+  u1 = {e[2], e[3]};
 }
 
 // b_0 of expand_message_xmd for an arbitrary-length message (bytes), DST bytes from dst_rt

@@ -17,8 +17,14 @@ __global__ void __launch_bounds__(TPB) k_fexp_step(const uint32_t* X, const uint
                                                    uint8_t* cls, uint32_t* OUT) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt || cls[i] != REJ_OK) return;
-  fp12 r = fexp_step<MODE>([&]() { return ld_fp12(X, cnt, i); }, [&]() { return ld_fp12(C, cnt, i); },
-                           [&]() { return ld_fp12(G, cnt, i); });
+  // the re-reads must stay at their use sites: an opaque copy of the index keeps LICM from hoisting
+  // them (a hoisted Fp12 would pin 144 VGPRs across the squaring loops)
+  auto at = [&](const uint32_t* B) {
+    size_t j = i;
+    asm volatile("" : "+v"(j));
+    return ld_fp12(B, cnt, j);
+  };
+  fp12 r = fexp_step<MODE>([&]() { return at(X); }, [&]() { return at(C); }, [&]() { return at(G); });
   if (MODE < 4) {
     st_fp12(OUT, cnt, i, r);
   } else if (!fp12_is_one(r)) {
