@@ -32,17 +32,12 @@ DI fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
 DI fp2 fp2_neg(const fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
 DI fp2 fp2_conj(const fp2& a) { return {a.c0, fp_neg(a.c1)}; }
 
-DI fp2 fp2_mul(const fp2& a, const fp2& b) {  // Karatsuba: 3 Fp mul
-  fp t0 = fp_mul(a.c0, b.c0);
-  fp t1 = fp_mul(a.c1, b.c1);
-  fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
-  return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
-}
+DI u24 fp2_to_u24(const fp2& a) { return u24_of(fp_to_u12(a.c0), fp_to_u12(a.c1)); }
+DI fp2 fp2_from_u24(const u24& v) { return {fp_from_u12(u24_lo(v)), fp_from_u12(u24_hi(v))}; }
 
-DI fp2 fp2_sqr(const fp2& a) {  // (a0+a1)(a0-a1), 2 a0 a1: 2 Fp mul
-  fp t = fp_mul(a.c0, a.c1);
-  return {fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1)), fp_dbl(t)};
-}
+// one fused call each (fp.h fp2_mul_u24 / fp2_sqr_u24): 3 and 2 Fp-mul equivalents
+DI fp2 fp2_mul(const fp2& a, const fp2& b) { return fp2_from_u24(fp2_mul_u24(fp2_to_u24(a), fp2_to_u24(b))); }
+DI fp2 fp2_sqr(const fp2& a) { return fp2_from_u24(fp2_sqr_u24(fp2_to_u24(a))); }
 
 DI fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
 DI fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1)}; }
