@@ -317,19 +317,50 @@ DI u24 u24_of(const u12& lo, const u12& hi) {
   return r;
 }
 
-// Fp2 product (a0 + a1 i)(b0 + b1 i) in one call: c0 = a0 b0 + a1 (p - b1), c1 = a0 b1 + a1 b0,
+// The second Fp2 operand of fp2_mul_u24 travels through LDS: 24 + 24 argument words exceed the 32
+// VGPR arguments of the AMDGPU calling convention (the excess would go through scratch). Each lane
+// owns one 24-word column of the block (kernels run 64-lane workgroups, kcommon.h TPB), and only
+// touches its own column, so no barrier is needed.
+constexpr int BLS_LANES = 64;
+#ifdef BLS_HOST
+static uint32_t g_fp2_arg[24 * BLS_LANES];
+DI unsigned bls_lane() { return 0; }
+#define BLS_SCHED_FENCE() ((void)0)
+#else
+static __shared__ uint32_t g_fp2_arg[24 * BLS_LANES];
+DI unsigned bls_lane() { return threadIdx.x; }
+// keeps the scheduler from interleaving two independent halves (it would double the callee's VGPRs)
+#define BLS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
+
+DI void fp2_arg_store(const u24& b) {
+  const unsigned l = bls_lane();
+#pragma unroll
+  for (int i = 0; i < 24; i++) g_fp2_arg[i * BLS_LANES + l] = b[i];
+}
+
+// Fp2 product (a0 + a1 i)(b0 + b1 i), b from fp2_arg_store, in one call:
+//   c0 = a0 b0 + a1 (p - b1), c1 = a0 b1 + a1 b0
 // i.e. two reductions instead of three multiplications' worth (counted as the 3 of Karatsuba).
-NOINL u24 fp2_mul_u24(u24 a, u24 b) {
+NOINL u24 fp2_mul_u24(u24 a) {
   BLS_COUNT_MUL();
   BLS_COUNT_MUL();
   BLS_COUNT_MUL();
+  const unsigned l = bls_lane();
+  u12 b0, b1;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    b0[i] = g_fp2_arg[i * BLS_LANES + l];
+    b1[i] = g_fp2_arg[(12 + i) * BLS_LANES + l];
+  }
   uint32_t x0[14], x1[14], y0[14], y1[14];
   fp_split28(u24_lo(a), x0);
   fp_split28(u24_hi(a), x1);
-  fp_split28(u24_lo(b), y0);
-  fp_split28(fp_p_minus_u12(u24_hi(b)), y1);
+  fp_split28(b0, y0);
+  fp_split28(fp_p_minus_u12(b1), y1);
   const u12 c0 = fp_mont_dot<true>(x0, y0, x1, y1);
-  fp_split28(u24_hi(b), y1);
+  BLS_SCHED_FENCE();
+  fp_split28(b1, y1);
   const u12 c1 = fp_mont_dot<true>(x0, y1, x1, y0);
   return u24_of(c0, c1);
 }
@@ -343,6 +374,7 @@ NOINL u24 fp2_sqr_u24(u24 a) {
   fp_split28(fp_add_raw_u12(a0, a1), x);
   fp_split28(fp_add_raw_u12(a0, fp_p_minus_u12(a1)), y);
   const u12 c0 = fp_mont_dot<false>(x, y, x, y);
+  BLS_SCHED_FENCE();
   fp_split28(fp_add_raw_u12(a0, a0), x);
   fp_split28(a1, y);
   const u12 c1 = fp_mont_dot<false>(x, y, x, y);

@@ -36,7 +36,10 @@ DI u24 fp2_to_u24(const fp2& a) { return u24_of(fp_to_u12(a.c0), fp_to_u12(a.c1)
 DI fp2 fp2_from_u24(const u24& v) { return {fp_from_u12(u24_lo(v)), fp_from_u12(u24_hi(v))}; }
 
 // one fused call each (fp.h fp2_mul_u24 / fp2_sqr_u24): 3 and 2 Fp-mul equivalents
-DI fp2 fp2_mul(const fp2& a, const fp2& b) { return fp2_from_u24(fp2_mul_u24(fp2_to_u24(a), fp2_to_u24(b))); }
+DI fp2 fp2_mul(const fp2& a, const fp2& b) {
+  fp2_arg_store(fp2_to_u24(b));
+  return fp2_from_u24(fp2_mul_u24(fp2_to_u24(a)));
+}
 DI fp2 fp2_sqr(const fp2& a) { return fp2_from_u24(fp2_sqr_u24(fp2_to_u24(a))); }
 
 DI fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
