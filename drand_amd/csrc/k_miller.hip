@@ -27,11 +27,7 @@ __global__ void __launch_bounds__(TPB) k_miller(const uint32_t* pk_tab, const ui
   Q[1].y = ld_fp2(S, cnt, i, 2);
   act[0] = !(pk_inf[k] | h_inf[i]);
   act[1] = !s_inf[i];
-#ifdef BLS_MILLER_SEPARATE_LINES
-  fp12 f = miller_loop_multi<2>(P, Q, act);
-#else
   fp12 f = miller_loop_2(P, Q, act);
-#endif
   st_fp12(F, cnt, i, f);
 }
 
