@@ -85,6 +85,7 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    from drand_amd import shard
     from drand_amd.engine import Engine
 
     g = load_json("tests/golden/golden.json")["chained"]  # fixed test key (sk, pk) of the golden chain
@@ -119,11 +120,7 @@ def main():
                                bitmap.data_ptr(), first_bad.data_ptr(), None, sp)
         if world > 1:
             # per-shard first bad ROUND -> global min; per-shard bitmaps -> every rank (RCCL over xGMI)
-            fb = first_bad.clone()
-            dist.all_reduce(fb, op=dist.ReduceOp.MIN)
-            gathered = torch.empty(world * words, dtype=torch.int64, device=dev)
-            dist.all_gather_into_tensor(gathered, bitmap)
-            return fb, gathered
+            return shard.combine(first_bad, bitmap, n, to_host=False)
         return first_bad, bitmap
 
     for _ in range(args.warmup):
@@ -134,7 +131,8 @@ def main():
     torch.cuda.synchronize(dev)
     ones = int(sum(bin(int(x) & (2 ** 64 - 1)).count("1") for x in bm.cpu().tolist()))
     fbv = int(fb.item()) & (2 ** 64 - 1)
-    assert fbv == 2 ** 64 - 1 and ones == n * world, f"verification failed: first_bad={fbv} ones={ones}"
+    assert fbv in (2 ** 64 - 1, shard.NONE_I64) and ones == n * world, \
+        f"verification failed: first_bad={fbv} ones={ones}"
 
     eng.profile(True)
     eng.profile_read()
