@@ -17,6 +17,7 @@
 namespace {
 
 constexpr size_t kMaxChunk = size_t(1) << 20;  // beacons per pipeline pass (~1 GB of staging)
+constexpr size_t kLineSub = size_t(1) << 17;   // Miller line staging: 128 Ki beacons x 39 KB = 5.1 GB
 
 struct DBuf {
   void* p = nullptr;
@@ -69,7 +70,7 @@ struct blsv_ctx {
   bool pk_cache_valid = false;
   // staging workspace
   size_t cap = 0;
-  DBuf H, S, F, FW, h_inf, s_inf, cls;
+  DBuf H, S, F, FW, LN, h_inf, s_inf, cls;
   // inputs / outputs
   DBuf in_sigs, in_msgs, in_off, in_len, in_rounds, seeds, bitmap, first_bad, sk, idx, lambdas, scratch, out,
       pp_tab, pp_inf, sel, g1_cls, misc;
@@ -99,6 +100,7 @@ static int ensure_workspace(blsv_ctx* c, size_t cnt) {
   HIPCHK(c, c->S.ensure(want * blsk::S_WORDS * 4));
   HIPCHK(c, c->F.ensure(want * blsk::F_WORDS * 4));
   HIPCHK(c, c->FW.ensure(3 * want * blsk::F_WORDS * 4));
+  HIPCHK(c, c->LN.ensure(std::min(want, kLineSub) * blsk::MILLER_LINE_WORDS * 4));
   HIPCHK(c, c->h_inf.ensure(want));
   HIPCHK(c, c->s_inf.ensure(want));
   HIPCHK(c, c->cls.ensure(want));
@@ -181,7 +183,8 @@ static int run_tail(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t of
   {
     StageTimer tm(c, ST_MILLER, cnt, st);
     blsk::launch_miller(pk.tab, pk.inf, pk.idx, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->S.as<uint32_t>(),
-                        c->s_inf.as<uint8_t>(), c->cls.as<uint8_t>(), cnt, c->F.as<uint32_t>(), st);
+                        c->s_inf.as<uint8_t>(), c->cls.as<uint8_t>(), cnt, c->F.as<uint32_t>(), c->LN.as<uint32_t>(),
+                        std::min(cnt, kLineSub), st);
   }
   {
     StageTimer tm(c, ST_FEXP, cnt, st);

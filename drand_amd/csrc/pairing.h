@@ -127,6 +127,50 @@ DI fp12 miller_loop_2(const g1a (&P)[2], const g2a (&Q)[2], const bool (&active)
   return fp12_conj(f);
 }
 
+// ---------------------------------------------------------------- staged Miller loop (device path)
+// The loop splits into two passes with a small live state each (k_miller.hip):
+//   lines : per pair, T runs through the 63 doublings + 5 additions and every line
+//           (3 Fp2) is written to HBM staging -- T (6 Fp) plus one step's temporaries live;
+//   f     : f = f^2 * (l_0 l_1) over the 68 steps, the lines re-read from staging -- f plus one
+//           line pair live.
+// Same lines, same products, same order as miller_loop_2 (tools/opcount checks f is identical).
+constexpr int MILLER_STEPS = 68;  // |x| = 0xd201000000010000: 63 doublings, 5 additions
+
+template <typename LoadQ, typename Emit>
+DI void miller_lines(const g1a& P, LoadQ load_q, Emit emit) {
+  const g2a Q0 = load_q();
+  g2proj T = {Q0.x, Q0.y, fp2_one()};
+  int step = 0;
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    line l;
+    miller_dbl_step(T, l.a0, l.a1, l.a4, P.x, P.y);
+    emit(step++, l);
+    if ((BLS_X_ABS >> i) & 1ull) {
+      miller_add_step(T, load_q(), l.a0, l.a1, l.a4, P.x, P.y);
+      emit(step++, l);
+    }
+  }
+}
+
+// load(step, k) returns pair k's line of that step (line_one() for a skipped pair)
+template <typename LoadLine>
+DI fp12 miller_f_from_lines(LoadLine load) {
+  fp12 f = fp12_one();
+  int step = 0;
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62) f = fp12_sqr(f);
+    f = fp12_mul_by_line_pair(f, line_mul_line(load(step, 0), load(step, 1)));
+    step++;
+    if ((BLS_X_ABS >> i) & 1ull) {
+      f = fp12_mul_by_line_pair(f, line_mul_line(load(step, 0), load(step, 1)));
+      step++;
+    }
+  }
+  return fp12_conj(f);
+}
+
 // single-pair form (test hook): same lines, f multiplied by each sparse line
 template <int NP>
 DI fp12 miller_loop_multi(const g1a (&P)[NP], const g2a (&Q)[NP], const bool (&active)[NP]) {

@@ -99,6 +99,19 @@ int main(int argc, char** argv) {
   fp12 f = miller_loop_2(Ps, Qs, act);
   unsigned long long n_miller = g_fp_mul_count - c0;
 
+  // the device's staged form (k_miller_lines + k_miller_f) must give the same f with the same work
+  {
+    static line lines[MILLER_STEPS][2];
+    const unsigned long long s0 = g_fp_mul_count;
+    for (int k = 0; k < 2; k++)
+      miller_lines(Ps[k], [&]() { return Qs[k]; }, [&](int step, const line& l) { lines[step][k] = l; });
+    fp12 fs = miller_f_from_lines([&](int step, int k) { return lines[step][k]; });
+    if (!fp12_eq(fs, f) || g_fp_mul_count - s0 != n_miller) {
+      printf("{\"verified\": false, \"staged_miller_mismatch\": true}\n");
+      return 1;
+    }
+  }
+
   c0 = g_fp_mul_count;
   bool ok = fp12_is_one(final_exponentiation(f));
   unsigned long long n_fexp = g_fp_mul_count - c0;
