@@ -27,7 +27,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-LIMB_PRODUCTS_PER_FP_MUL = 288  # CIOS 12x32-bit Montgomery: 144 (a*b) + 144 (m*p) v_mad_u64_u32
+LIMB_PRODUCTS_PER_FP_MUL = 288  # algorithmic unit: 12x32-bit Montgomery = 144 (a*b) + 144 (m*p) limb products
+PMC_FILE = "r01_pmc_traffic.json"
 
 
 def load_json(rel):
@@ -171,6 +172,11 @@ def main():
     d = stages[dom]
     achieved = opc[dom] * LIMB_PRODUCTS_PER_FP_MUL * d["items_per_launch"] / (d["ms_per_launch"] * 1e-3) / 1e12
     peak = peak_info["peak_mad_u64_u32_per_s"] / 1e12
+    try:  # HBM bytes per beacon of each stage from the committed PMC passes (tools/pmc_traffic.py)
+        tb = load_json("profiles/" + PMC_FILE)["bytes_per_beacon"][dom]["total"]
+        traffic = round(tb * d["items_per_launch"])
+    except (FileNotFoundError, KeyError):
+        traffic = None
     per_beacon_fp_mul = sum(opc.values())
 
     out = {
@@ -190,7 +196,8 @@ def main():
                                % n, "beacons_per_gpu": n, "segment_len": seg, "parallelism": "range-shard x%d" % world},
         "roofline": {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
                      "unit": "T limb-products/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4),
-                     "traffic": None,
+                     "traffic": traffic,
+                     "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/%s)" % PMC_FILE if traffic else None,
                      "algorithmic_limb_products_per_beacon": per_beacon_fp_mul * LIMB_PRODUCTS_PER_FP_MUL,
                      "whole_pipeline_frac": round(value / world * per_beacon_fp_mul * LIMB_PRODUCTS_PER_FP_MUL
                                                   / (peak * 1e12), 4)},

@@ -4,7 +4,7 @@
 
 namespace blsk {
 
-__global__ void __launch_bounds__(TPB) k_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, size_t base,
+BLS_KERNEL(BLS_WPE_DECOMP) k_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, size_t base,
                                                        size_t cnt, uint32_t* S, uint8_t* s_inf, uint8_t* cls) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt) return;

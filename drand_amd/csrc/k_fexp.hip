@@ -6,14 +6,14 @@
 
 namespace blsk {
 
-__global__ void __launch_bounds__(TPB) k_fexp_easy(const uint32_t* F, size_t cnt, const uint8_t* cls, uint32_t* G) {
+BLS_KERNEL(BLS_WPE_FEXP) k_fexp_easy(const uint32_t* F, size_t cnt, const uint8_t* cls, uint32_t* G) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt || cls[i] != REJ_OK) return;
   st_fp12(G, cnt, i, fexp_easy(ld_fp12(F, cnt, i)));
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(TPB) k_fexp_step(const uint32_t* X, const uint32_t* C, const uint32_t* G, size_t cnt,
+BLS_KERNEL(BLS_WPE_FEXP) k_fexp_step(const uint32_t* X, const uint32_t* C, const uint32_t* G, size_t cnt,
                                                    uint8_t* cls, uint32_t* OUT) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt || cls[i] != REJ_OK) return;

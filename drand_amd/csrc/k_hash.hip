@@ -15,7 +15,7 @@ DI void store_h(uint32_t* H, uint8_t* h_inf, size_t cnt, size_t i, const g2j& h)
   h_inf[i] = inf;
 }
 
-__global__ void __launch_bounds__(TPB) k_hash_chained(ChainedSrc src, size_t base, size_t cnt, uint32_t* H,
+BLS_KERNEL(BLS_WPE_HASH) k_hash_chained(ChainedSrc src, size_t base, size_t cnt, uint32_t* H,
                                                       uint8_t* h_inf) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt) return;
@@ -36,7 +36,7 @@ __global__ void __launch_bounds__(TPB) k_hash_chained(ChainedSrc src, size_t bas
   store_h(H, h_inf, cnt, i, hash_to_g2(msg));
 }
 
-__global__ void __launch_bounds__(TPB) k_hash_unchained(const uint64_t* rounds, uint64_t first_round, size_t base,
+BLS_KERNEL(BLS_WPE_HASH) k_hash_unchained(const uint64_t* rounds, uint64_t first_round, size_t base,
                                                         size_t cnt, uint32_t* H, uint8_t* h_inf) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt) return;
@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(TPB) k_hash_unchained(const uint64_t* rounds, 
   store_h(H, h_inf, cnt, i, hash_to_g2(msg));
 }
 
-__global__ void __launch_bounds__(TPB) k_hash_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len,
+BLS_KERNEL(BLS_WPE_HASH) k_hash_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len,
                                                        size_t cnt, uint32_t* H, uint8_t* h_inf) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt) return;

@@ -7,17 +7,13 @@
 // kilic Engine.AddPair / AddPairInv [ext] via kyber-bls12381 ValidatePairing.
 #include "kcommon.h"
 
-#ifndef BLS_LINES_WAVES_PER_EU
-#define BLS_LINES_WAVES_PER_EU 2
-#endif
-
 namespace blsk {
 
 // line slot of (step, pair): 6 Fp slots (a0, a1, a4 as Fp2)
 DI int line_slot(int step, int k) { return (step * 2 + k) * 6; }
 
 // Item g = base + i of the chunk (H/S/F/cls stride cnt); its lines at LN index i (stride sub).
-__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(BLS_LINES_WAVES_PER_EU)))
+BLS_KERNEL(BLS_WPE_LINES)
 k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
                const uint8_t* h_inf, const uint32_t* S, const uint8_t* s_inf, const uint8_t* cls, size_t cnt,
                size_t base, size_t m, size_t sub, uint32_t* LN) {
@@ -57,7 +53,7 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
   }
 }
 
-__global__ void __launch_bounds__(TPB) k_miller_f(const uint32_t* LN, const uint8_t* cls, size_t cnt, size_t base,
+BLS_KERNEL(BLS_WPE_MILLER_F) k_miller_f(const uint32_t* LN, const uint8_t* cls, size_t cnt, size_t base,
                                                   size_t m, size_t sub, uint32_t* F) {
   const size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= m) return;

@@ -12,4 +12,24 @@ constexpr int TPB = 64;  // one wave per workgroup: register-heavy lanes, many w
 
 static inline unsigned grid_for(size_t n) { return (unsigned)((n + TPB - 1) / TPB); }
 
+// Waves per SIMD each stage kernel is compiled for (amdgpu_waves_per_eu caps its VGPR budget at
+// 512 / n). 1 = the full 512 VGPR+AGPR budget; 2 = 256 VGPRs, twice the resident waves, some
+// spilling. Chosen per stage from A/B runs on the MI355X (scripts/gpu_variants.sh).
+#ifndef BLS_WPE_HASH
+#define BLS_WPE_HASH 1
+#endif
+#ifndef BLS_WPE_DECOMP
+#define BLS_WPE_DECOMP 2
+#endif
+#ifndef BLS_WPE_LINES
+#define BLS_WPE_LINES 2
+#endif
+#ifndef BLS_WPE_MILLER_F
+#define BLS_WPE_MILLER_F 1
+#endif
+#ifndef BLS_WPE_FEXP
+#define BLS_WPE_FEXP 1
+#endif
+#define BLS_KERNEL(wpe) __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(wpe)))
+
 }  // namespace blsk

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 TAG=${1:-iter}
 timeout -k 10 400 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1 || exit 12
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit 13
-timeout -k 10 500 python -u bench.py --steps 3 --warmup 1 --cpu-per-worker 1 > gpurun_out/${TAG}_bench.log 2>&1 || exit 14
+timeout -k 10 500 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1 || exit 14
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace -o run -- python -u bench.py --n 262144 --steps 2 --warmup 1 --cpu-per-worker 0 > gpurun_out/${TAG}_trace.log 2>&1 || exit 15
 if [ -n "$PMC" ]; then
   i=0

@@ -1,0 +1,121 @@
+"""GPU parity at scale: device-generated chained histories (the bench workload, BASELINE.json
+configs[1]/[4]) checked through size-independent properties, with samples cross-checked by the C
+oracle (oracle/c/bls_oracle.c, pinned to the reference KAT in tests/test_oracle_c.py):
+
+  * every generated round verifies (bitmap all ones, first_bad = none), also across pipeline-chunk
+    boundaries and for ragged sizes;
+  * a corrupted signature i rejects exactly rounds i and i+1 (chain.VerifyBeacon hashes the given
+    PreviousSig bytes, chain/beacon.go:87-108) unless i+1 starts a new segment; first_bad is the
+    smallest rejected ROUND; reject classes match the C oracle;
+  * V2 (unchained) batches signed on device verify, wrong rounds reject.
+"""
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NONE = (1 << 64) - 1
+
+
+@pytest.fixture(scope="module")
+def C():
+    from oracle import c_oracle
+
+    if not os.path.exists(c_oracle.LIB_PATH):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    c_oracle.load()
+    return c_oracle
+
+
+def _history(engine, golden, n, seg, first_round=1, seed=7):
+    import torch
+
+    ch = golden["chained"]
+    engine.set_public_key(bytes.fromhex(ch["pk"]))
+    sk32 = int(ch["sk"], 16).to_bytes(32, "big")
+    n_seg = (n + seg - 1) // seg
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(seed)
+    seeds = torch.randint(0, 256, (n_seg * 96,), dtype=torch.uint8, device="cuda:0", generator=g)
+    sigs = torch.empty(n * 96, dtype=torch.uint8, device="cuda:0")
+    seed0_len = 32 if first_round == 1 else 96
+    engine.generate_chained_dev(sk32, first_round, seg, seeds.data_ptr(), seed0_len, sigs.data_ptr(), n)
+    torch.cuda.synchronize()
+    return seeds, sigs, seed0_len
+
+
+def _verify(engine, first_round, seg, seeds, seed0_len, sigs, n):
+    import torch
+
+    words = (n + 63) // 64
+    bitmap = torch.zeros(words, dtype=torch.int64, device="cuda:0")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda:0")
+    cls = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    engine.verify_chained_dev(first_round, seg, seeds.data_ptr(), seed0_len, sigs.data_ptr(), n, bitmap.data_ptr(),
+                              fb.data_ptr(), cls.data_ptr())
+    torch.cuda.synchronize()
+    bm = [w & NONE for w in bitmap.cpu().tolist()]
+    ok = [(bm[i // 64] >> (i % 64)) & 1 == 1 for i in range(n)]
+    return ok, int(fb.item()) & NONE, cls.cpu().tolist()
+
+
+def _segments(seeds, sigs, seed0_len, seg, first_round, idx):
+    """(first_round, prev0, sigs) chained pieces covering the segments that contain the indices idx"""
+    sh = sigs.cpu().numpy().tobytes()
+    sd = seeds.cpu().numpy().tobytes()
+    n = len(sh) // 96
+    out = []
+    for s in sorted({i // seg for i in idx}):
+        lo, hi = s * seg, min(n, (s + 1) * seg)
+        prev0 = sd[s * 96: s * 96 + (seed0_len if s == 0 else 96)]
+        out.append((lo, first_round + lo, prev0, sh[lo * 96: hi * 96]))
+    return out
+
+
+@pytest.mark.parametrize("n,seg", [(4099, 64), (1 << 20 | 4099, 64)])
+def test_generated_history_all_accept(engine, golden, C, n, seg):
+    seeds, sigs, s0 = _history(engine, golden, n, seg)
+    ok, fb, cls = _verify(engine, 1, seg, seeds, s0, sigs, n)
+    assert all(ok) and fb == NONE and not any(cls)
+    # the generator agrees with the C oracle: first segment, one across the 2^20 chunk edge, last
+    pk48 = bytes.fromhex(golden["chained"]["pk"])
+    for lo, fr, prev0, sg in _segments(seeds, sigs, s0, seg, 1, [0, min(n - 1, (1 << 20) - 1), n - 1]):
+        assert C.verify_chained(pk48, fr, prev0, sg[: 8 * 96]) == [0] * min(8, len(sg) // 96)
+
+
+def test_corrupted_history_rejects_exactly(engine, golden, C):
+    import torch
+
+    n, seg = 20000, 64
+    seeds, sigs, s0 = _history(engine, golden, n, seg, seed=11)
+    bad = [5, 127, 128, 4000, 12345, n - 1]  # 127: next round starts a segment; 128: a segment start
+    host = sigs.cpu()
+    for k, i in enumerate(bad):
+        host[i * 96 + 40 + k] ^= 0x10  # flip a bit of x (c1)
+    sigs.copy_(host.to("cuda:0"))
+    ok, fb, cls = _verify(engine, 1, seg, seeds, s0, sigs, n)
+    want = set(bad) | {i + 1 for i in bad if i + 1 < n and (i + 1) % seg != 0}
+    assert {i for i, v in enumerate(ok) if not v} == want
+    assert fb == 1 + min(want)
+    pk48 = bytes.fromhex(golden["chained"]["pk"])
+    for lo, fr, prev0, sg in _segments(seeds, sigs, s0, seg, 1, sorted(want)):
+        want_cls = C.verify_chained(pk48, fr, prev0, sg)
+        assert cls[lo: lo + len(want_cls)] == want_cls
+
+
+def test_unchained_batch_signed_on_device(engine, golden):
+    ch = golden["chained"]
+    engine.set_public_key(bytes.fromhex(ch["pk"]))
+    sk32 = int(ch["sk"], 16).to_bytes(32, "big")
+    import hashlib
+
+    n, first = 3000, 1_000_000
+    msgs = [hashlib.sha256((first + i).to_bytes(8, "big")).digest() for i in range(n)]  # chain.MessageV2
+    sigs = engine.sign(sk32, msgs)
+    res = engine.verify_unchained(sigs, first_round=first)
+    assert all(res.ok) and res.first_bad is None
+    res = engine.verify_unchained(sigs, first_round=first + 1)
+    assert not any(res.ok) and res.first_bad == first + 1
