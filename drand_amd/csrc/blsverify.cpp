@@ -174,7 +174,7 @@ struct PkSel {
 
 static int run_tail(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t offset, size_t base, size_t cnt,
                     const PkSel& pk, uint64_t* d_bitmap, unsigned long long* d_first_bad, uint8_t* d_cls_out,
-                    hipStream_t st) {
+                    hipStream_t st, uint64_t label0 = 0) {
   {
     StageTimer tm(c, ST_DECOMP, cnt, st);
     blsk::launch_decompress_g2(d_sigs, stride, offset, base, cnt, c->S.as<uint32_t>(), c->s_inf.as<uint8_t>(),
@@ -192,7 +192,7 @@ static int run_tail(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t of
   }
   {
     StageTimer tm(c, ST_FINISH, cnt, st);
-    blsk::launch_finish(c->cls.as<uint8_t>(), base, cnt, d_bitmap, d_first_bad, st);
+    blsk::launch_finish(c->cls.as<uint8_t>(), base, cnt, d_bitmap, d_first_bad, label0, st);
   }
   if (d_cls_out) HIPCHK(c, hipMemcpyAsync(d_cls_out + base, c->cls.p, cnt, hipMemcpyDeviceToDevice, st));
   HIPCHK(c, hipGetLastError());
@@ -576,7 +576,7 @@ int blsv_verify_chained_dev(blsv_ctx* c, uint64_t first_round, uint64_t seg_len,
       blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), st);
     }
     rc = run_tail(c, d_sigs96, 96, 0, base, cnt, group_pk(c), d_bitmap, (unsigned long long*)d_first_bad,
-                  d_reject_class, st);
+                  d_reject_class, st, first_round);  // d_first_bad holds a ROUND (include/blsverify.h)
     if (rc) return rc;
   }
   return BLSV_OK;

@@ -25,8 +25,10 @@ BLS_KERNEL(BLS_WPE_DECOMP) k_decompress_g2(const uint8_t* sigs, size_t stride, s
   cls[i] = c;
 }
 
+// first_bad receives label0 + (index of the first reject): label0 = first_round gives the ROUND
+// (chained device batches), 0 the batch index (host entry points add their own round mapping).
 __global__ void __launch_bounds__(256) k_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap,
-                                                unsigned long long* first_bad) {
+                                                unsigned long long* first_bad, uint64_t label0) {
   size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   const bool in = i < cnt;
   const bool ok = in && cls[i] == REJ_OK;
@@ -38,7 +40,7 @@ __global__ void __launch_bounds__(256) k_finish(const uint8_t* cls, size_t base,
   const size_t wave0 = i - lane;
   if (lane == 0 && wave0 < cnt) {
     bitmap[(base + wave0) >> 6] = okm;
-    if (badm) atomicMin(first_bad, (unsigned long long)(base + wave0 + __builtin_ctzll(badm)));
+    if (badm) atomicMin(first_bad, (unsigned long long)(label0 + base + wave0 + __builtin_ctzll(badm)));
   }
 }
 
@@ -51,10 +53,10 @@ void launch_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, siz
 }
 
 void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap, unsigned long long* first_bad,
-                   hipStream_t st) {
+                   uint64_t label0, hipStream_t st) {
   if (!cnt) return;
   hipLaunchKernelGGL(k_finish, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, cls, base, cnt, bitmap,
-                     first_bad);
+                     first_bad, label0);
 }
 
 }  // namespace blsk

@@ -47,9 +47,10 @@ void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t
                    uint32_t* F, uint32_t* LN, size_t sub, hipStream_t st);
 // F is clobbered; W = 3 * cnt * F_WORDS words of staging
 void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st);
-// bitmap bit (base+i) = (cls[i] == 0); bitmap must cover whole 64-bit words; first_bad = min index
+// bitmap bit (base+i) = (cls[i] == 0); bitmap must cover whole 64-bit words;
+// first_bad = label0 + min rejected index (label0 = first_round -> ROUND numbers)
 void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap, unsigned long long* first_bad,
-                   hipStream_t st);
+                   uint64_t label0, hipStream_t st);
 
 // ---- group / threshold / signing kernels (k_misc.hip)
 // decompress cnt G1 points (48 B each) -> pk table entries + inf flags + reject class
