@@ -97,6 +97,16 @@ DI fp fp_add(const fp& a, const fp& b) {
 
 DI fp fp_dbl(const fp& a) { return fp_add(a, a); }
 
+// a + b WITHOUT reduction, for inputs < 2p: the result (< 4p) may only feed a multiplier (see the
+// operand contract above fp_mul_u12), never fp_add/fp_sub/fp_eq or serialization.
+DI fp fp_add_lazy(const fp& a, const fp& b) {
+  fp r;
+  unsigned c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = __builtin_addc(a.l[i], b.l[i], c, &c);
+  return r;
+}
+
 // a/2 mod p: (a + (a odd ? p : 0)) >> 1 (the sum is < 2p < 2^382, no 13th limb needed)
 DI fp fp_half(const fp& a) {
   const uint32_t m = 0u - (a.l[0] & 1u);
@@ -139,6 +149,10 @@ DI fp fp_neg(const fp& a) {
 
 typedef uint32_t u12 __attribute__((ext_vector_type(12)));
 
+// Operand contract of the multipliers (fp_mul_u12, fp_sqr_u12, fp2_mul_u24, fp2_sqr_u24): every
+// input word-vector may be any value < 4p ("lazily reduced": the sum of two values < 2p, see
+// fp_add_lazy), outputs are canonical in [0, p). With inputs < 4p a Montgomery dot product of two
+// terms is < 2 * (8p)^2 = 128 p^2 < 2^769, so the result (< 2^377 + p) needs one subtraction.
 // Montgomery product a*b*R^-1 mod p, R = 2^392.
 // Deliberately NOT inlined: one copy of the body per code object keeps kernels small
 // (instruction-cache resident) and compile times sane. Arguments/results are ext_vector u12 so
@@ -245,12 +259,12 @@ NOINL u12 fp_sqr_u12(u12 a) {
   return fp_join28_reduce(t);
 }
 
-// p - a for a in [0, p] (12-word borrow chain)
-DI u12 fp_p_minus_u12(const u12& a) {
+// 4p - a for a in [0, 4p] (12-word borrow chain): -a mod p for a lazily-reduced operand
+DI u12 fp_4p_minus_u12(const u12& a) {
   u12 r;
   unsigned br = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) r[i] = __builtin_subc(P_RAW[i], a[i], br, &br);
+  for (int i = 0; i < 12; i++) r[i] = __builtin_subc(P4_RAW[i], a[i], br, &br);
   return r;
 }
 
@@ -340,7 +354,7 @@ DI void fp2_arg_store(const u24& b) {
 }
 
 // Fp2 product (a0 + a1 i)(b0 + b1 i), b from fp2_arg_store, in one call:
-//   c0 = a0 b0 + a1 (p - b1), c1 = a0 b1 + a1 b0
+//   c0 = a0 b0 + a1 (4p - b1), c1 = a0 b1 + a1 b0
 // i.e. two reductions instead of three multiplications' worth (counted as the 3 of Karatsuba).
 NOINL u24 fp2_mul_u24(u24 a) {
   BLS_COUNT_MUL();
@@ -357,7 +371,7 @@ NOINL u24 fp2_mul_u24(u24 a) {
   fp_split28(u24_lo(a), x0);
   fp_split28(u24_hi(a), x1);
   fp_split28(b0, y0);
-  fp_split28(fp_p_minus_u12(b1), y1);
+  fp_split28(fp_4p_minus_u12(b1), y1);
   const u12 c0 = fp_mont_dot<true>(x0, y0, x1, y1);
   BLS_SCHED_FENCE();
   fp_split28(b1, y1);
@@ -365,14 +379,14 @@ NOINL u24 fp2_mul_u24(u24 a) {
   return u24_of(c0, c1);
 }
 
-// Fp2 square: c0 = (a0 + a1)(a0 + p - a1), c1 = (2 a0) a1
+// Fp2 square: c0 = (a0 + a1)(a0 + 4p - a1), c1 = (2 a0) a1
 NOINL u24 fp2_sqr_u24(u24 a) {
   BLS_COUNT_MUL();
   BLS_COUNT_MUL();
   const u12 a0 = u24_lo(a), a1 = u24_hi(a);
   uint32_t x[14], y[14];
   fp_split28(fp_add_raw_u12(a0, a1), x);
-  fp_split28(fp_add_raw_u12(a0, fp_p_minus_u12(a1)), y);
+  fp_split28(fp_add_raw_u12(a0, fp_4p_minus_u12(a1)), y);
   const u12 c0 = fp_mont_dot<false>(x, y, x, y);
   BLS_SCHED_FENCE();
   fp_split28(fp_add_raw_u12(a0, a0), x);

@@ -35,7 +35,7 @@ DI void miller_dbl_step(g2proj& t, fp2& l00, fp2& l01, fp2& l11, const fp& xp, c
   fp2 E = fp2_mul_3b(C);
   fp2 F = fp2_mul3(E);
   fp2 G = fp2_half(fp2_add(B, F));
-  fp2 H = fp2_sub(fp2_sqr(fp2_add(t.y, t.z)), fp2_add(B, C));
+  fp2 H = fp2_sub(fp2_sqr(fp2_add_lazy(t.y, t.z)), fp2_add(B, C));
   fp2 X2 = fp2_sqr(t.x);
   l00 = fp2_sub(E, B);
   l01 = fp2_mul_fp(fp2_mul3(X2), xp);
@@ -71,16 +71,16 @@ struct line {
 //   c0 = (a0 b0 + xi a4 b4, a0 b1 + a1 b0, a1 b1),  c1 = (0, a0 b4 + a4 b0, a1 b4 + a4 b1)
 DI fp12 line_mul_line(const line& a, const line& b) {
   fp2 t00 = fp2_mul(a.a0, b.a0), t11 = fp2_mul(a.a1, b.a1), t44 = fp2_mul(a.a4, b.a4);
-  fp2 c01 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.a0, a.a1), fp2_add(b.a0, b.a1)), t00), t11);
-  fp2 c11 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.a0, a.a4), fp2_add(b.a0, b.a4)), t00), t44);
-  fp2 c12 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.a1, a.a4), fp2_add(b.a1, b.a4)), t11), t44);
+  fp2 c01 = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.a0, a.a1), fp2_add_lazy(b.a0, b.a1)), t00), t11);
+  fp2 c11 = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.a0, a.a4), fp2_add_lazy(b.a0, b.a4)), t00), t44);
+  fp2 c12 = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.a1, a.a4), fp2_add_lazy(b.a1, b.a4)), t11), t44);
   return {{fp2_add(t00, fp2_mul_xi(t44)), c01, t11}, {fp2_zero(), c11, c12}};
 }
 
 // a * (b1 v + b2 v^2) (5 Fp2 mul)
 DI fp6 fp6_mul_by_12(const fp6& a, const fp2& b1, const fp2& b2) {
   fp2 t1 = fp2_mul(a.c1, b1), t2 = fp2_mul(a.c2, b2);
-  fp2 m = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b1, b2)), t1), t2);  // a1 b2 + a2 b1
+  fp2 m = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c1, a.c2), fp2_add_lazy(b1, b2)), t1), t2);  // a1 b2 + a2 b1
   return {fp2_mul_xi(m), fp2_add(fp2_mul(a.c0, b1), fp2_mul_xi(t2)), fp2_add(fp2_mul(a.c0, b2), t1)};
 }
 
@@ -88,8 +88,8 @@ DI fp6 fp6_mul_by_12(const fp6& a, const fp2& b1, const fp2& b2) {
 DI fp12 fp12_mul_by_line_pair(const fp12& f, const fp12& L) {
   fp6 t0 = fp6_mul(f.c0, L.c0);
   fp6 t1 = fp6_mul_by_12(f.c1, L.c1.c1, L.c1.c2);
-  fp6 Ls = {L.c0.c0, fp2_add(L.c0.c1, L.c1.c1), fp2_add(L.c0.c2, L.c1.c2)};
-  fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(f.c0, f.c1), Ls), t0), t1);
+  fp6 Ls = {L.c0.c0, fp2_add_lazy(L.c0.c1, L.c1.c1), fp2_add_lazy(L.c0.c2, L.c1.c2)};
+  fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add_lazy(f.c0, f.c1), Ls), t0), t1);
   return {fp6_add(t0, fp6_mul_v(t1)), c1};
 }
 

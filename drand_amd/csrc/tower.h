@@ -27,6 +27,8 @@ DI bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) & fp_is_zero(a.c1); 
 DI bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) & fp_eq(a.c1, b.c1); }
 DI fp2 fp2_select(bool c, const fp2& a, const fp2& b) { return {fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
 DI fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+// unreduced sum (< 4p for inputs < 2p): only as a multiplier operand (fp.h operand contract)
+DI fp2 fp2_add_lazy(const fp2& a, const fp2& b) { return {fp_add_lazy(a.c0, b.c0), fp_add_lazy(a.c1, b.c1)}; }
 DI fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
 DI fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
 DI fp2 fp2_neg(const fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
@@ -124,17 +126,22 @@ DI fp6 fp6_mul(const fp6& a, const fp6& b) {  // Karatsuba, 6 Fp2 mul
   fp2 t0 = fp2_mul(a.c0, b.c0);
   fp2 t1 = fp2_mul(a.c1, b.c1);
   fp2 t2 = fp2_mul(a.c2, b.c2);
-  fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), t1), t2)), t0);
-  fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), t0), t1), fp2_mul_xi(t2));
-  fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), t0), t2), t1);
+  fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c1, a.c2), fp2_add_lazy(b.c1, b.c2)), t1), t2)), t0);
+  fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(b.c0, b.c1)), t0), t1), fp2_mul_xi(t2));
+  fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c2), fp2_add_lazy(b.c0, b.c2)), t0), t2), t1);
   return {c0, c1, c2};
+}
+
+// fp6 sum for a multiplier input (fp6_mul / fp6_mul_by_* take operands < 2p per coefficient)
+DI fp6 fp6_add_lazy(const fp6& a, const fp6& b) {
+  return {fp2_add_lazy(a.c0, b.c0), fp2_add_lazy(a.c1, b.c1), fp2_add_lazy(a.c2, b.c2)};
 }
 
 DI fp6 fp6_sqr(const fp6& a) {  // CH-SQR2
   fp2 s0 = fp2_sqr(a.c0);
   fp2 ab = fp2_mul(a.c0, a.c1);
   fp2 s1 = fp2_dbl(ab);
-  fp2 s2 = fp2_sqr(fp2_add(fp2_sub(a.c0, a.c1), a.c2));
+  fp2 s2 = fp2_sqr(fp2_add_lazy(fp2_sub(a.c0, a.c1), a.c2));
   fp2 bc = fp2_mul(a.c1, a.c2);
   fp2 s3 = fp2_dbl(bc);
   fp2 s4 = fp2_sqr(a.c2);
@@ -148,9 +155,9 @@ DI fp6 fp6_sqr(const fp6& a) {  // CH-SQR2
 DI fp6 fp6_mul_by_01(const fp6& a, const fp2& b0, const fp2& b1) {
   fp2 t0 = fp2_mul(a.c0, b0);
   fp2 t1 = fp2_mul(a.c1, b1);
-  fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), b1), t1)), t0);
-  fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), t0), t1);
-  fp2 c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), b0), t0), t1);
+  fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_mul(fp2_add_lazy(a.c1, a.c2), b1), t1)), t0);
+  fp2 c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(b0, b1)), t0), t1);
+  fp2 c2 = fp2_add(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c2), b0), t0), t1);
   return {c0, c1, c2};
 }
 
@@ -177,14 +184,14 @@ DI fp12 fp12_conj(const fp12& a) { return {a.c0, fp6_neg(a.c1)}; }  // a^(p^6)
 DI fp12 fp12_mul(const fp12& a, const fp12& b) {  // Karatsuba, 3 Fp6 mul
   fp6 t0 = fp6_mul(a.c0, b.c0);
   fp6 t1 = fp6_mul(a.c1, b.c1);
-  fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), t0), t1);
+  fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add_lazy(a.c0, a.c1), fp6_add_lazy(b.c0, b.c1)), t0), t1);
   fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
   return {c0, c1};
 }
 
 DI fp12 fp12_sqr(const fp12& a) {  // complex squaring, 2 Fp6 mul
   fp6 ab = fp6_mul(a.c0, a.c1);
-  fp6 t = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  fp6 t = fp6_mul(fp6_add_lazy(a.c0, a.c1), fp6_add_lazy(a.c0, fp6_mul_v(a.c1)));
   fp6 c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab));
   fp6 c1 = fp6_add(ab, ab);
   return {c0, c1};
@@ -194,7 +201,7 @@ DI fp12 fp12_sqr(const fp12& a) {  // complex squaring, 2 Fp6 mul
 DI fp12 fp12_mul_by_014(const fp12& f, const fp2& l00, const fp2& l01, const fp2& l11) {
   fp6 a = fp6_mul_by_01(f.c0, l00, l01);
   fp6 b = fp6_mul_by_1(f.c1, l11);
-  fp6 c = fp6_mul_by_01(fp6_add(f.c0, f.c1), l00, fp2_add(l01, l11));
+  fp6 c = fp6_mul_by_01(fp6_add_lazy(f.c0, f.c1), l00, fp2_add_lazy(l01, l11));
   fp6 c1 = fp6_sub(fp6_sub(c, a), b);
   fp6 c0 = fp6_add(a, fp6_mul_v(b));
   return {c0, c1};
@@ -207,7 +214,7 @@ DI void fp4_sqr(fp2& c0, fp2& c1, const fp2& a, const fp2& b) {
   fp2 t0 = fp2_sqr(a);
   fp2 t1 = fp2_sqr(b);
   c0 = fp2_add(fp2_mul_xi(t1), t0);
-  c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add(a, b)), t0), t1);
+  c1 = fp2_sub(fp2_sub(fp2_sqr(fp2_add_lazy(a, b)), t0), t1);
 }
 
 DI fp12 fp12_cyclotomic_sqr(const fp12& f) {

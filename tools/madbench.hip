@@ -5,7 +5,30 @@
 #include <stdint.h>
 #include <stdio.h>
 
-#define MAD(acc, x, y, cc) asm volatile("v_mad_u64_u32 %0, " cc ", %1, %2, %0" : "+v"(acc) : "v"(x), "v"(y) : "s0", "s1", "s2", "s3", "s4", "s5", "s6", "s7", "vcc")
+#define MAD8(c0, c1, c2, c3, c4, c5, c6, c7)                                                            \
+  asm volatile("v_mad_u64_u32 %0, " c0 ", %8, %9, %0\n\t"                                               \
+               "v_mad_u64_u32 %1, " c1 ", %8, %9, %1\n\t"                                               \
+               "v_mad_u64_u32 %2, " c2 ", %8, %9, %2\n\t"                                               \
+               "v_mad_u64_u32 %3, " c3 ", %8, %9, %3\n\t"                                               \
+               "v_mad_u64_u32 %4, " c4 ", %8, %9, %4\n\t"                                               \
+               "v_mad_u64_u32 %5, " c5 ", %8, %9, %5\n\t"                                               \
+               "v_mad_u64_u32 %6, " c6 ", %8, %9, %6\n\t"                                               \
+               "v_mad_u64_u32 %7, " c7 ", %8, %9, %7"                                                   \
+               : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)         \
+               : "v"(x), "v"(y)                                                                         \
+               : "s0", "s1", "s2", "s3", "s4", "s5", "s6", "s7", "vcc")
+#define DEP8(c0, c1, c2, c3, c4, c5, c6, c7)                                                             \
+  asm volatile("v_mad_u64_u32 %0, " c0 ", %1, %2, %0\n\t"                                               \
+               "v_mad_u64_u32 %0, " c1 ", %1, %2, %0\n\t"                                               \
+               "v_mad_u64_u32 %0, " c2 ", %1, %2, %0\n\t"                                               \
+               "v_mad_u64_u32 %0, " c3 ", %1, %2, %0\n\t"                                               \
+               "v_mad_u64_u32 %0, " c4 ", %1, %2, %0\n\t"                                               \
+               "v_mad_u64_u32 %0, " c5 ", %1, %2, %0\n\t"                                               \
+               "v_mad_u64_u32 %0, " c6 ", %1, %2, %0\n\t"                                               \
+               "v_mad_u64_u32 %0, " c7 ", %1, %2, %0"                                                   \
+               : "+v"(a0)                                                                               \
+               : "v"(x), "v"(y)                                                                         \
+               : "s0", "s1", "s2", "s3", "s4", "s5", "s6", "s7", "vcc")
 
 template <int MODE>
 __global__ void __launch_bounds__(64) k_mad(const uint32_t* in, uint64_t* out, int iters) {
@@ -14,19 +37,10 @@ __global__ void __launch_bounds__(64) k_mad(const uint32_t* in, uint64_t* out, i
   for (int it = 0; it < iters; it++) {
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-      if (MODE == 0) {  // same SGPR pair
-        MAD(a0, x, y, "s[0:1]"); MAD(a1, x, y, "s[0:1]"); MAD(a2, x, y, "s[0:1]"); MAD(a3, x, y, "s[0:1]");
-        MAD(a4, x, y, "s[0:1]"); MAD(a5, x, y, "s[0:1]"); MAD(a6, x, y, "s[0:1]"); MAD(a7, x, y, "s[0:1]");
-      } else if (MODE == 1) {  // rotating pairs
-        MAD(a0, x, y, "s[0:1]"); MAD(a1, x, y, "s[2:3]"); MAD(a2, x, y, "s[4:5]"); MAD(a3, x, y, "s[6:7]");
-        MAD(a4, x, y, "s[0:1]"); MAD(a5, x, y, "s[2:3]"); MAD(a6, x, y, "s[4:5]"); MAD(a7, x, y, "s[6:7]");
-      } else if (MODE == 2) {  // vcc
-        MAD(a0, x, y, "vcc"); MAD(a1, x, y, "vcc"); MAD(a2, x, y, "vcc"); MAD(a3, x, y, "vcc");
-        MAD(a4, x, y, "vcc"); MAD(a5, x, y, "vcc"); MAD(a6, x, y, "vcc"); MAD(a7, x, y, "vcc");
-      } else {  // one dependent chain
-        MAD(a0, x, y, "s[0:1]"); MAD(a0, x, y, "s[2:3]"); MAD(a0, x, y, "s[4:5]"); MAD(a0, x, y, "s[6:7]");
-        MAD(a0, x, y, "s[0:1]"); MAD(a0, x, y, "s[2:3]"); MAD(a0, x, y, "s[4:5]"); MAD(a0, x, y, "s[6:7]");
-      }
+      if (MODE == 0) MAD8("s[0:1]", "s[0:1]", "s[0:1]", "s[0:1]", "s[0:1]", "s[0:1]", "s[0:1]", "s[0:1]");
+      if (MODE == 1) MAD8("s[0:1]", "s[2:3]", "s[4:5]", "s[6:7]", "s[0:1]", "s[2:3]", "s[4:5]", "s[6:7]");
+      if (MODE == 2) MAD8("vcc", "vcc", "vcc", "vcc", "vcc", "vcc", "vcc", "vcc");
+      if (MODE == 3) DEP8("s[0:1]", "s[2:3]", "s[4:5]", "s[6:7]", "s[0:1]", "s[2:3]", "s[4:5]", "s[6:7]");
     }
   }
   out[blockIdx.x * 64 + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
