@@ -204,7 +204,7 @@ def main():
         "stages_ms_per_launch": {s: round(v["ms_per_launch"], 3) for s, v in stages.items()},
         "generate_s": round(t_gen, 2),
     }
-    if rank == 0 and args.cpu_per_worker > 0:
+    if rank == 0 and world == 1 and args.cpu_per_worker > 0:  # CPU baseline: rank 0 at N=1 only
         # bounded sample of the same workload: the first whole segments of the rank-0 shard
         workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
         n_seg_cpu = min(n_seg, max(1, (workers * args.cpu_per_worker + seg - 1) // seg))

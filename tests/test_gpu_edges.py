@@ -1,0 +1,89 @@
+"""GPU edge cases through the C ABI, each checked against the Python oracle or the goldens:
+empty and ragged batches, wrong-length inputs (rejected host-side, grpcserver.go:66-69), the
+point-at-infinity rules of kilic's pairing engine (O pairs are skipped, empty product = 1), and
+tbls Recover's share selection (first t VALID shares in input order, duplicates keep the first,
+fewer than t valid -> error; the group signature a0*H(m) is the same for every valid t-subset)."""
+import random
+
+import pytest
+
+from drand_amd import _lib
+from drand_amd.engine import EngineError
+from oracle import bls12381 as O
+
+pytestmark = pytest.mark.gpu
+
+INF_G1 = bytes([0xC0]) + bytes(47)
+INF_G2 = bytes([0xC0]) + bytes(95)
+
+
+def test_empty_batches(engine, golden):
+    ch = golden["chained"]
+    engine.set_public_key(bytes.fromhex(ch["pk"]))
+    res = engine.verify_chained(1, bytes.fromhex(ch["genesis_seed"]), [])
+    assert res.ok == [] and res.first_bad is None
+    res = engine.verify_unchained([], first_round=1)
+    assert res.ok == [] and res.first_bad is None
+    assert engine.verify_messages([], []).ok == []
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65])
+def test_ragged_chained_prefixes(engine, golden, n):
+    ch = golden["chained"]
+    engine.set_public_key(bytes.fromhex(ch["pk"]))
+    sigs = [bytes.fromhex(b["sig"]) for b in ch["beacons"]]
+    seed = bytes.fromhex(ch["genesis_seed"])
+    reps = (n + len(sigs) - 1) // len(sigs)
+    # beyond the golden chain: rounds past the end reject (their messages differ) -- prefix only
+    m = min(n, len(sigs))
+    res = engine.verify_chained(1, seed, sigs[:m])
+    assert all(res.ok) and len(res.ok) == m
+    if n > len(sigs):  # a ragged batch of n: the golden chain twice; the second copy rejects
+        batch = (sigs * reps)[:n]
+        res = engine.verify_chained(1, seed, batch)
+        assert all(res.ok[:len(sigs)]) and not any(res.ok[len(sigs):])
+        assert res.first_bad == len(sigs) + 1
+
+
+def test_wrong_length_rejected_host_side(engine, golden):
+    ch = golden["chained"]
+    engine.set_public_key(bytes.fromhex(ch["pk"]))
+    with pytest.raises(ValueError):
+        engine.verify_chained(1, bytes.fromhex(ch["genesis_seed"]), [bytes(3)])  # grpcserver.go:66-69
+    with pytest.raises(ValueError):
+        engine.verify_unchained([b""], first_round=1)
+
+
+def test_infinity_rules_match_oracle(engine, golden):
+    kat = golden["kat"]
+    msg = bytes.fromhex(kat["msg"])
+    sig = bytes.fromhex(kat["sig"])
+    cases = [(bytes.fromhex(kat["pk"]), INF_G2),  # valid pk, sigma = O: e(pk, H) != 1 -> reject
+             (INF_G1, INF_G2),                    # both pairs skipped: empty product -> kilic accepts
+             (INF_G1, sig)]                       # only e(-g1, sigma) left -> reject
+    for pk48, s in cases:
+        pk = O.g1_decompress(pk48)
+        want = O.verify_class(pk, msg, s)
+        res = engine.verify_messages([msg], [s], pk48=pk48)
+        assert res.reject_class == [want], (pk48[:1].hex(), s[:1].hex())
+
+
+def test_recover_selection_rules(engine, golden):
+    th = golden["threshold"]
+    engine.set_group([bytes.fromhex(c) for c in th["commits"]], th["n"])
+    msg = bytes.fromhex(th["msg"])
+    partials = [bytes.fromhex(p) for p in th["partials"]]
+    t = th["t"]
+    rng = random.Random(9)
+    for _ in range(2):  # any t valid shares give the same group signature
+        sub = rng.sample(partials, t)
+        assert engine.recover(msg, sub, t, th["n"]).hex() == th["group_sig"]
+    bad = bytes.fromhex(th["bad_partial"])
+    dup = partials[0]
+    # invalid shares and duplicate indices are skipped, the next valid ones complete the set
+    sub = [bad, dup, dup] + partials[1:t]
+    assert engine.recover(msg, sub, t, th["n"]).hex() == th["group_sig"]
+    # fewer than t valid shares -> BLSV_ENOTENOUGH
+    with pytest.raises(EngineError) as e:
+        engine.recover(msg, [bad] + partials[: t - 1], t, th["n"])
+    assert e.value.code == _lib.BLSV_ENOTENOUGH
