@@ -1,0 +1,141 @@
+"""Offline verification of a node's stored history: drand.db → SoA → batched GPU verify.
+
+SURVEY.md §8f rank 2. ``libboltload.so`` (drand_amd/csrc/boltload.cpp, include/boltload.h) walks
+bucket "beacons" of the bbolt file (chain/boltdb/store.go:21,68-81) and decodes every hexjson
+``chain.Beacon`` straight into round / prev / signature arrays. ``verify_store`` then splits the
+arrays into linked runs with numpy (round + 1 and ``PreviousSig == previous Signature``, the
+``appendStore.Put`` rule of chain/beacon/store.go:43-48) and hands each run to
+``Engine.verify_chained_packed``; each beacon's verdict is ``chain.VerifyBeacon``
+(chain/beacon.go:87-92) on its own stored fields.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from .callers import _verify_run
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libboltload.so")
+_lib = None
+
+
+class StoreError(RuntimeError):
+    pass
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise StoreError(f"{LIB_PATH} not found: build with make -C drand_amd/csrc")
+        lib = ctypes.CDLL(LIB_PATH)
+        vp, sz, u8 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p
+        lib.dl_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(vp)]
+        lib.dl_open.restype = ctypes.c_int
+        lib.dl_count.argtypes = [vp]
+        lib.dl_count.restype = ctypes.c_int64
+        lib.dl_load.argtypes = [vp, sz, sz, u8, u8, u8, u8, u8, u8, u8, ctypes.POINTER(sz)]
+        lib.dl_load.restype = ctypes.c_int
+        lib.dl_last_error.argtypes = [vp]
+        lib.dl_last_error.restype = ctypes.c_char_p
+        lib.dl_close.argtypes = [vp]
+        lib.dl_close.restype = None
+        _lib = lib
+    return _lib
+
+
+@dataclass
+class StoredBeacons:
+    """SoA view of bucket "beacons": n rows in round order. Byte fields are zero-padded to 96;
+    ``*_len`` give the stored lengths (255 = longer than 96)."""
+    rounds: np.ndarray      # uint64[n]
+    prev: np.ndarray        # uint8[n, 96]
+    prev_len: np.ndarray    # uint8[n]
+    sigs: np.ndarray        # uint8[n, 96]
+    sig_len: np.ndarray     # uint8[n]
+    sigs_v2: np.ndarray     # uint8[n, 96]
+    v2_len: np.ndarray      # uint8[n]
+
+    def __len__(self):
+        return len(self.rounds)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def load_store(path, start=0, max_n=None) -> StoredBeacons:
+    """Read entries [start, start + max_n) of bucket "beacons" (all of them by default)."""
+    lib = _load()
+    h = ctypes.c_void_p()
+    rc = lib.dl_open(os.fsencode(path), ctypes.byref(h))
+    try:
+        if rc != 0:
+            raise StoreError(lib.dl_last_error(h).decode() if h.value else "dl_open failed")
+        total = lib.dl_count(h)
+        n = max(0, total - start) if max_n is None else max(0, min(max_n, total - start))
+        out = StoredBeacons(np.zeros(n, np.uint64), np.zeros((n, 96), np.uint8), np.zeros(n, np.uint8),
+                            np.zeros((n, 96), np.uint8), np.zeros(n, np.uint8), np.zeros((n, 96), np.uint8),
+                            np.zeros(n, np.uint8))
+        got = ctypes.c_size_t()
+        if n:
+            rc = lib.dl_load(h, start, n, _ptr(out.rounds), _ptr(out.prev), _ptr(out.prev_len), _ptr(out.sigs),
+                             _ptr(out.sig_len), _ptr(out.sigs_v2), _ptr(out.v2_len), ctypes.byref(got))
+            if rc != 0:
+                raise StoreError(lib.dl_last_error(h).decode())
+        return out
+    finally:
+        if h.value:
+            lib.dl_close(h)
+
+
+def linked_runs(sb: StoredBeacons):
+    """Start indices of maximal runs that ``blsv_verify_chained`` can take in one call."""
+    n = len(sb)
+    if n == 0:
+        return np.zeros(0, np.int64)
+    link = np.zeros(n, bool)
+    if n > 1:
+        link[1:] = ((sb.rounds[1:] == sb.rounds[:-1] + 1) & (sb.prev_len[1:] == 96) & (sb.sig_len[:-1] == 96)
+                    & (sb.sig_len[1:] == 96) & np.all(sb.prev[1:] == sb.sigs[:-1], axis=1))
+    return np.flatnonzero(~link)
+
+
+@dataclass
+class StoreVerdict:
+    ok: np.ndarray              # bool[n], in stored (round) order
+    first_bad: int | None       # lowest failing round, None if every beacon verifies
+    runs: int                   # engine calls made for the linked runs
+
+
+def verify_store(engine, public_key: bytes, sb: StoredBeacons) -> StoreVerdict:
+    """``chain.VerifyBeacon`` for every stored beacon, one GPU call per linked run."""
+    engine.set_public_key(public_key)
+    n = len(sb)
+    ok = np.zeros(n, bool)
+    starts = linked_runs(sb)
+    ends = np.append(starts[1:], n)
+    for s, e in zip(starts.tolist(), ends.tolist()):
+        plen = int(sb.prev_len[s])
+        prev0 = sb.prev[s, :plen].tobytes() if plen <= 96 else None
+        if int(sb.sig_len[s]) != 96 or prev0 is None or plen not in (32, 96):
+            # a lone malformed first beacon: kyber rejects a non-96-byte signature; an odd-length
+            # (or over-long) stored prev is still a well-defined message -> message-form call
+            if prev0 is None or int(sb.sig_len[s]) != 96:
+                ok[s] = False
+                s0 = s + 1
+            else:
+                ok[s] = _verify_run(engine, int(sb.rounds[s]), prev0, [sb.sigs[s].tobytes()]) is None
+                s0 = s + 1
+            if s0 < e:
+                res = engine.verify_chained_packed(int(sb.rounds[s0]), sb.prev[s0].tobytes(),
+                                                   np.ascontiguousarray(sb.sigs[s0:e]), e - s0)
+                ok[s0:e] = res.ok
+            continue
+        res = engine.verify_chained_packed(int(sb.rounds[s]), prev0, np.ascontiguousarray(sb.sigs[s:e]), e - s)
+        ok[s:e] = res.ok
+    bad = np.flatnonzero(~ok)
+    return StoreVerdict(ok, int(sb.rounds[bad[0]]) if len(bad) else None, len(starts))

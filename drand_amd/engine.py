@@ -108,6 +108,20 @@ class Engine:
                                                  bm, ctypes.byref(fb), cls))
         return BatchResult(_bits(bm, n), None if fb.value == 2 ** 64 - 1 else fb.value, list(cls)[:n])
 
+    def verify_chained_packed(self, first_round, prev0, sigs96, n):
+        """``verify_chained`` over n signatures already packed as n*96 contiguous bytes (any object
+        with the buffer protocol, e.g. a numpy slice of the bulk loader's SoA array)."""
+        mv = memoryview(sigs96).cast("B")
+        if len(mv) != 96 * n:
+            raise ValueError("packed signatures must be n*96 bytes")
+        bm = _lib.out_buf((n + 7) // 8)
+        fb = ctypes.c_uint64()
+        cls = _lib.out_buf(n)
+        src = (ctypes.c_uint8 * max(len(mv), 1)).from_buffer_copy(mv) if len(mv) else None
+        self._check(self.lib.blsv_verify_chained(self._h, first_round, _lib.buf(prev0), len(prev0), src, n, bm,
+                                                 ctypes.byref(fb), cls))
+        return BatchResult(_bits(bm, n), None if fb.value == 2 ** 64 - 1 else fb.value, list(cls)[:n])
+
     def verify_unchained(self, sigs, first_round=None, rounds=None):
         n = len(sigs)
         if any(len(s) != 96 for s in sigs):

@@ -38,6 +38,19 @@ def test_library_exports_every_symbol():
     assert b"gfx950" in lib.blsv_version()
 
 
+def test_boltload_exports_every_symbol():
+    """include/boltload.h (drand.db bulk loader) against libboltload.so."""
+    from drand_amd import boltdb
+    if not os.path.exists(boltdb.LIB_PATH):
+        pytest.skip("libboltload.so not built (run __graft_entry__.build())")
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "boltload.h")).read(), flags=re.S)
+    syms = set(re.findall(r"\b(dl_\w+)\s*\(", txt))
+    assert syms == {"dl_open", "dl_count", "dl_load", "dl_last_error", "dl_close"}
+    lib = ctypes.CDLL(boltdb.LIB_PATH)
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
 def test_engine_refuses_without_library(monkeypatch, tmp_path):
     """No CPU fallback: a missing library is a loud error."""
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
