@@ -19,7 +19,10 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -139,12 +142,18 @@ int find_bucket(dl_db* db, const uint8_t* p, const char* name, int depth) {
     return 1;  // not here
 }
 
-int hexval(int c) {
-    if (c >= '0' && c <= '9') return c - '0';
-    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
-    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
-    return -1;
-}
+struct HexLut {
+    int8_t v[256];
+    HexLut() {
+        for (int c = 0; c < 256; c++) v[c] = -1;
+        for (int c = '0'; c <= '9'; c++) v[c] = int8_t(c - '0');
+        for (int c = 'a'; c <= 'f'; c++) v[c] = int8_t(c - 'a' + 10);
+        for (int c = 'A'; c <= 'F'; c++) v[c] = int8_t(c - 'A' + 10);
+    }
+};
+const HexLut kHex;
+
+inline int hexval(uint8_t c) { return kHex.v[c]; }
 
 // Decode a hex string value into out (cap bytes); returns byte length, or -1 on malformed hex.
 long hexdecode(const uint8_t* s, size_t n, uint8_t* out, size_t cap) {
@@ -266,33 +275,76 @@ int dl_open(const char* path, dl_db** out) {
 
 int64_t dl_count(const dl_db* db) { return db ? int64_t(db->entries.size()) : -1; }
 
+}  // extern "C"
+
+namespace {
+
+// Decode entries [lo, hi) into row i - start; returns the first failing entry index or -1.
+long decode_range(dl_db* db, size_t start, size_t lo, size_t hi, uint64_t* rounds, uint8_t* prev96,
+                  uint8_t* prev_len, uint8_t* sigs96, uint8_t* sig_len, uint8_t* sigs_v2_96, uint8_t* v2_len,
+                  std::string& err) {
+    uint8_t scratch[96];
+    for (size_t j = lo; j < hi; j++) {
+        size_t i = j - start;
+        const Entry& en = db->entries[j];
+        Fields f;
+        uint8_t* v2 = sigs_v2_96 ? sigs_v2_96 + 96 * i : scratch;
+        std::memset(prev96 + 96 * i, 0, 96);
+        std::memset(sigs96 + 96 * i, 0, 96);
+        if (sigs_v2_96) std::memset(v2, 0, 96);
+        if (parse_beacon(en.v, en.vs, f, prev96 + 96 * i, sigs96 + 96 * i, v2)) {
+            err = "malformed beacon JSON at entry " + std::to_string(j);
+            return long(j);
+        }
+        if (en.ks != 8) {
+            err = "key is not an 8-byte round at entry " + std::to_string(j);
+            return long(j);
+        }
+        uint64_t key = 0;
+        for (int b = 0; b < 8; b++) key = key << 8 | en.k[b];
+        if (key != f.round) {
+            err = "key round " + std::to_string(key) + " != value round " + std::to_string(f.round);
+            return long(j);
+        }
+        rounds[i] = f.round;
+        // lengths above 96 are reported as 255 ("not a signature"); the bytes kept are the first 96
+        prev_len[i] = uint8_t(f.prev_len > 96 ? 255 : f.prev_len);
+        sig_len[i] = uint8_t(f.sig_len > 96 ? 255 : f.sig_len);
+        if (v2_len) v2_len[i] = uint8_t(f.v2_len > 96 ? 255 : f.v2_len);
+    }
+    return -1;
+}
+
+}  // namespace
+
+extern "C" {
+
 int dl_load(dl_db* db, size_t start, size_t max_n, uint64_t* rounds, uint8_t* prev96, uint8_t* prev_len,
             uint8_t* sigs96, uint8_t* sig_len, uint8_t* sigs_v2_96, uint8_t* v2_len, size_t* n_out) {
     if (!db || !n_out || !rounds || !prev96 || !prev_len || !sigs96 || !sig_len) return -1;
     *n_out = 0;
     if (start > db->entries.size()) return fail(db, "start beyond the last entry");
     size_t n = std::min(max_n, db->entries.size() - start);
-    uint8_t scratch[96];
-    for (size_t i = 0; i < n; i++) {
-        const Entry& en = db->entries[start + i];
-        Fields f;
-        uint8_t* v2 = sigs_v2_96 ? sigs_v2_96 + 96 * i : scratch;
-        std::memset(prev96 + 96 * i, 0, 96);
-        std::memset(sigs96 + 96 * i, 0, 96);
-        if (sigs_v2_96) std::memset(v2, 0, 96);
-        if (parse_beacon(en.v, en.vs, f, prev96 + 96 * i, sigs96 + 96 * i, v2))
-            return fail(db, "malformed beacon JSON at entry " + std::to_string(start + i));
-        if (en.ks != 8) return fail(db, "key is not an 8-byte round at entry " + std::to_string(start + i));
-        uint64_t key = 0;
-        for (int b = 0; b < 8; b++) key = key << 8 | en.k[b];
-        if (key != f.round)
-            return fail(db, "key round " + std::to_string(key) + " != value round " + std::to_string(f.round));
-        rounds[i] = f.round;
-        // lengths above 96 are clamped to 255 as "not a signature"; the bytes kept are the first 96
-        prev_len[i] = uint8_t(f.prev_len > 96 ? 255 : f.prev_len);
-        sig_len[i] = uint8_t(f.sig_len > 96 ? 255 : f.sig_len);
-        if (v2_len) v2_len[i] = uint8_t(f.v2_len > 96 ? 255 : f.v2_len);
+    // The values are independent: decode in parallel, contiguous slices per thread (the mmap'd
+    // pages are read once; the SoA rows each thread writes are disjoint).
+    unsigned hw = std::thread::hardware_concurrency();
+    size_t nt = std::max<size_t>(1, std::min<size_t>({size_t(hw ? hw : 1), 16, (n + 16383) / 16384}));
+    if (const char* e = std::getenv("DL_THREADS")) nt = std::max<size_t>(1, size_t(std::atoi(e)));
+    std::vector<long> bad(nt, -1);
+    std::vector<std::string> errs(nt);
+    std::vector<std::thread> pool;
+    size_t per = (n + nt - 1) / nt;
+    for (size_t t = 0; t < nt; t++) {
+        size_t lo = start + std::min(n, t * per), hi = start + std::min(n, (t + 1) * per);
+        auto job = [=, &bad, &errs] {
+            bad[t] = decode_range(db, start, lo, hi, rounds, prev96, prev_len, sigs96, sig_len, sigs_v2_96, v2_len,
+                                  errs[t]);
+        };
+        if (nt == 1) job(); else pool.emplace_back(job);
     }
+    for (auto& th : pool) th.join();
+    for (size_t t = 0; t < nt; t++)
+        if (bad[t] >= 0) return fail(db, errs[t]);   // lowest slice first = lowest failing entry
     *n_out = n;
     return 0;
 }

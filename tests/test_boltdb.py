@@ -118,3 +118,20 @@ def test_verify_store_cpu(tmp_path, chain):
 @pytest.mark.gpu
 def test_verify_store_gpu(tmp_path, chain, engine):
     _check_verdicts(engine, tmp_path, chain)
+
+
+def test_parallel_decode_reports_lowest_bad_entry(tmp_path, chain, monkeypatch):
+    _, _, bs = chain
+    items = _items(bs) * 2
+    items = [(struct.pack(">Q", i + 1), ingest.beacon_to_json(Beacon(b.previous_sig, i + 1, b.signature)))
+             for i, (_, v) in enumerate(items) for b in [ingest.beacon_from_json(v)]]
+    items[35] = (items[35][0], b'{"Round":36,"Signature":"0g"}')
+    items[30] = (items[30][0], b'{"Round":31,"PreviousSig":"abc"}')
+    p = tmp_path / "par.db"
+    write_db(p, items, per_leaf=2)
+    monkeypatch.setenv("DL_THREADS", "4")
+    with pytest.raises(boltdb.StoreError, match="entry 30"):
+        boltdb.load_store(p)
+    monkeypatch.setenv("DL_THREADS", "3")
+    sb = boltdb.load_store(p, start=0, max_n=30)
+    assert sb.rounds.tolist() == list(range(1, 31))
