@@ -1,0 +1,139 @@
+"""Measurements for BASELINE.json configs[2] and configs[4] on one MI355X (bench.py covers configs[1]).
+
+configs[2] threshold round: n = 64 / t = 33 partials of the golden threshold fixture. One aggregator
+round of chain/beacon/chain.go:119-166 = verify all 64 partials (node.go:112) + Recover from 33 +
+VerifyRecovered of the group signature. Reports the median wall-clock latency per round.
+
+configs[4] mixed batch: a device-generated 1M-round chained history (bench.py's layout: segments of
+64 rounds, golden key) with a seeded 0.1 % of signatures corrupted on device (bit flip in x, cleared
+compression flag, infinity encoding, x >= p, a valid signature of another round). The verdict
+bitmap must equal the expectation exactly: a corrupted sig_i rejects round i and, inside its
+segment, round i + 1 (whose message hashes the corrupted bytes); first_bad = the minimum. Reports
+beacons/s over the mixed batch.
+
+Prints one JSON line. Usage: python tools/config_bench.py [--n 1000000] [--reps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def threshold_round(eng, th, reps):
+    commits = [bytes.fromhex(c) for c in th["commits"]]
+    msg = bytes.fromhex(th["msg"])
+    partials = [bytes.fromhex(p) for p in th["partials"]]
+    sub = [bytes.fromhex(p) for p in th["recover_subset"]]
+    eng.set_group(commits, th["n"])
+    lat = []
+    for k in range(reps + 2):
+        t0 = time.perf_counter()
+        ok, _ = eng.verify_partials(msg, partials)
+        sig = eng.recover(msg, sub, th["t"], th["n"])
+        res = eng.verify_messages([msg], [sig])
+        dt = time.perf_counter() - t0
+        assert all(ok) and res.ok == [True] and sig.hex() == th["group_sig"]
+        if k >= 2:
+            lat.append(dt * 1e3)
+    return {"n": th["n"], "t": th["t"], "median_ms_per_round": round(statistics.median(lat), 3),
+            "min_ms": round(min(lat), 3), "reps": reps, "bit_exact_group_sig": True}
+
+
+def mixed_batch(eng, g, n, seg, steps):
+    import torch
+    dev = torch.device("cuda", 0)
+    sk32 = int(g["sk"], 16).to_bytes(32, "big")
+    eng.set_public_key(bytes.fromhex(g["pk"]))
+    n_seg = (n + seg - 1) // seg
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0x5EED5)
+    seeds = torch.randint(0, 256, (n_seg * 96,), dtype=torch.uint8, device=dev, generator=gen)
+    sigs = torch.empty(n * 96, dtype=torch.uint8, device=dev)
+    bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    first_bad = torch.empty(1, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    eng.generate_chained_dev(sk32, 1, seg, seeds.data_ptr(), 32, sigs.data_ptr(), n, sp)
+    torch.cuda.synchronize(dev)
+
+    rng = torch.Generator()
+    rng.manual_seed(1234)
+    k = max(1, n // 1000)
+    idx = torch.randperm(n, generator=rng)[:k].sort().values
+    s2 = sigs.view(n, 96)
+    p_bytes = bytes.fromhex("1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab")
+    p_t = torch.tensor(list(p_bytes), dtype=torch.uint8, device=dev)
+    kinds = {}
+    for j, i in enumerate(idx.tolist()):
+        kind = j % 5
+        kinds[kind] = kinds.get(kind, 0) + 1
+        if kind == 0:                                       # bit flip in x
+            s2[i, 60] ^= 0x10
+        elif kind == 1:                                     # compression flag cleared
+            s2[i, 0] &= 0x7F
+        elif kind == 2:                                     # infinity encoding (valid point, fails pairing)
+            s2[i].zero_()
+            s2[i, 0] = 0xC0
+        elif kind == 3:                                     # x.c0 = p (non-canonical)
+            s2[i, 48:96] = p_t
+        else:                                               # a valid signature of another round
+            s2[i] = s2[(i + 7) % n].clone()
+    torch.cuda.synchronize(dev)
+    bad = set(idx.tolist())
+    expect_bad = set(bad)
+    for i in bad:
+        if i + 1 < n and (i + 1) % seg != 0:
+            expect_bad.add(i + 1)
+
+    def step():
+        eng.verify_chained_dev(1, seg, seeds.data_ptr(), 32, sigs.data_ptr(), n, bitmap.data_ptr(),
+                               first_bad.data_ptr(), None, sp)
+
+    step()
+    torch.cuda.synchronize(dev)
+    bm = bitmap.cpu().numpy().view("uint64")
+    import numpy as np
+    bits = np.unpackbits(bm.view(np.uint8), bitorder="little")[:n]
+    got_bad = set(np.flatnonzero(bits == 0).tolist())
+    assert got_bad == expect_bad, (len(got_bad), len(expect_bad))
+    fb = int(first_bad.item()) & (2 ** 64 - 1)
+    assert fb == min(expect_bad) + 1, (fb, min(expect_bad) + 1)   # first_bad is a ROUND (round = index + 1)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    return {"n": n, "segment_len": seg, "corrupted": k, "rejected": len(expect_bad), "kinds": kinds,
+            "bitmap_exact": True, "first_bad_round": fb, "beacons_per_s": round(n * steps / dt, 1),
+            "ms_per_batch": round(dt * 1e3 / steps, 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--seg-len", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)   # initialise torch's HIP runtime before the engine's context (as bench.py does)
+    torch.zeros(1, device="cuda")
+    from drand_amd.engine import Engine
+    with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+        golden = json.load(f)
+    eng = Engine(0)
+    out = {"configs[2]_threshold_round": threshold_round(eng, golden["threshold"], args.reps),
+           "configs[4]_mixed_batch": mixed_batch(eng, golden["chained"], args.n, args.seg_len, args.steps)}
+    print(json.dumps(out))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
