@@ -123,7 +123,9 @@ def verify_store(engine, public_key: bytes, sb: StoredBeacons) -> StoreVerdict:
         prev0 = sb.prev[s, :plen].tobytes() if plen <= 96 else None
         if int(sb.sig_len[s]) != 96 or prev0 is None or plen not in (32, 96):
             # a lone malformed first beacon: kyber rejects a non-96-byte signature; an odd-length
-            # (or over-long) stored prev is still a well-defined message -> message-form call
+            # stored prev is still a well-defined message -> message-form call. A prev longer than
+            # 96 bytes is not kept by the loader and is reported as a reject (documented deviation:
+            # no drand writer produces one).
             if prev0 is None or int(sb.sig_len[s]) != 96:
                 ok[s] = False
                 s0 = s + 1
@@ -139,3 +141,50 @@ def verify_store(engine, public_key: bytes, sb: StoredBeacons) -> StoreVerdict:
         ok[s:e] = res.ok
     bad = np.flatnonzero(~ok)
     return StoreVerdict(ok, int(sb.rounds[bad[0]]) if len(bad) else None, len(starts))
+
+
+def store_count(path) -> int:
+    """Entries in bucket "beacons" (boltStore.Len, chain/boltdb/store.go:47-58)."""
+    lib = _load()
+    h = ctypes.c_void_p()
+    try:
+        if lib.dl_open(os.fsencode(path), ctypes.byref(h)) != 0:
+            raise StoreError(lib.dl_last_error(h).decode() if h.value else "dl_open failed")
+        return int(lib.dl_count(h))
+    finally:
+        if h.value:
+            lib.dl_close(h)
+
+
+def _words(ok: np.ndarray) -> np.ndarray:
+    """bool[n] -> int64 words, bit i = ok[i], LSB first (the kernels' bitmap layout)."""
+    n = len(ok)
+    padded = np.zeros(((n + 63) // 64) * 64, np.uint8)
+    padded[:n] = ok
+    return np.packbits(padded, bitorder="little").view(np.int64)
+
+
+def verify_store_sharded(engine, public_key: bytes, path, device=None, group=None):
+    """Multi-GPU offline check of one store (SURVEY.md §8e applied to §8f rank 2).
+
+    Each rank loads and verifies a contiguous slice of the stored entries (``shard.shard_range``).
+    No halo is needed: every stored beacon carries its own PreviousSig. The exchange is
+    ``shard.combine``: one MIN all-reduce of the first bad round and one all-gather of the bitmaps.
+    Returns (global first bad round or None, global ok bool array in stored order)."""
+    import torch
+    import torch.distributed as dist
+
+    from . import shard
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    sh = shard.shard_range(store_count(path), world, rank)
+    sb = load_store(path, start=sh.start, max_n=sh.count)
+    v = verify_store(engine, public_key, sb)
+    words = torch.from_numpy(_words(v.ok).copy())
+    if device is not None:
+        words = words.to(device)
+    fb, gwords = shard.combine(shard.NONE_U64 if v.first_bad is None else v.first_bad, words, sh.count,
+                               group=group)
+    total = sum(shard.shard_range(store_count(path), world, r).count for r in range(world))
+    bits = np.unpackbits(np.array(gwords, dtype=np.uint64).view(np.uint8), bitorder="little")[:total]
+    return (None if fb == shard.NONE_U64 else fb), bits.astype(bool)

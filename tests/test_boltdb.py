@@ -135,3 +135,43 @@ def test_parallel_decode_reports_lowest_bad_entry(tmp_path, chain, monkeypatch):
     monkeypatch.setenv("DL_THREADS", "3")
     sb = boltdb.load_store(p, start=0, max_n=30)
     assert sb.rounds.tolist() == list(range(1, 31))
+
+
+def _sharded_worker(rank, world, port, path, pk, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fb, ok = boltdb.verify_store_sharded(OracleEngine(), pk, path)
+        q.put((rank, fb, ok.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_verify_store_sharded_gloo(tmp_path, chain, world):
+    """Row (e) over row (f): ranks split the stored entries, combine with MIN + all-gather (gloo)."""
+    import multiprocessing as mp
+    import socket
+    pk, _, bs = chain
+    p = tmp_path / "s.db"
+    tb = _tampered(bs)
+    write_db(p, _items(tb), per_leaf=4)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, str(p), pk, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    rounds = [b.round for b in tb]
+    want = [r not in (10, 16) for r in rounds]
+    for _, fb, ok in res:
+        assert fb == 10 and ok == want
