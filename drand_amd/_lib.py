@@ -54,6 +54,7 @@ SIGNATURES = {
     "blsv_synchronize": (ctypes.c_int, [vp]),
     "blsv_set_group": (ctypes.c_int, [vp, u8p, sz, sz]),
     "blsv_verify_chained": (ctypes.c_int, [vp, ctypes.c_uint64, u8p, sz, u8p, sz, u8p, u64p, u8p]),
+    "blsv_verify_prevs": (ctypes.c_int, [vp, ctypes.c_uint64, u8p, sz, u8p, sz, u8p, u64p, u8p]),
     "blsv_verify_unchained": (ctypes.c_int, [vp, u64p, ctypes.c_uint64, u8p, sz, u8p, u64p, u8p]),
     "blsv_verify_messages": (ctypes.c_int, [vp, u8p, u8p, u32p, sz, u8p, u8p, u64p, u8p]),
     "blsv_verify_partials": (ctypes.c_int, [vp, u8p, sz, u8p, sz, sz, u8p, u8p]),

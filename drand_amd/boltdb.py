@@ -2,11 +2,11 @@
 
 SURVEY.md §8f rank 2. ``libboltload.so`` (drand_amd/csrc/boltload.cpp, include/boltload.h) walks
 bucket "beacons" of the bbolt file (chain/boltdb/store.go:21,68-81) and decodes every hexjson
-``chain.Beacon`` straight into round / prev / signature arrays. ``verify_store`` then splits the
-arrays into linked runs with numpy (round + 1 and ``PreviousSig == previous Signature``, the
-``appendStore.Put`` rule of chain/beacon/store.go:43-48) and hands each run to
-``Engine.verify_chained_packed``; each beacon's verdict is ``chain.VerifyBeacon``
-(chain/beacon.go:87-92) on its own stored fields.
+``chain.Beacon`` straight into round / prev / signature arrays. ``verify_store`` hands each run of
+consecutive rounds to ``Engine.verify_prevs`` (one device pass, every row hashing its own stored
+PreviousSig); each beacon's verdict is ``chain.VerifyBeacon`` (chain/beacon.go:87-92) on its own
+stored fields. ``linked_runs`` reports the ``appendStore.Put`` linkage rule
+(chain/beacon/store.go:43-48: round + 1 and ``PreviousSig == previous Signature``).
 """
 from __future__ import annotations
 
@@ -111,34 +111,43 @@ class StoreVerdict:
     runs: int                   # engine calls made for the linked runs
 
 
+def round_runs(sb: StoredBeacons):
+    """Start indices of maximal runs of consecutive rounds in which every row but the first has a
+    96-byte PreviousSig: each is one device pass (``Engine.verify_prevs``), whatever the linkage."""
+    n = len(sb)
+    if n == 0:
+        return np.zeros(0, np.int64)
+    cont = np.zeros(n, bool)
+    if n > 1:
+        cont[1:] = (sb.rounds[1:] == sb.rounds[:-1] + 1) & (sb.prev_len[1:] == 96)
+    return np.flatnonzero(~cont)
+
+
 def verify_store(engine, public_key: bytes, sb: StoredBeacons) -> StoreVerdict:
-    """``chain.VerifyBeacon`` for every stored beacon, one GPU call per linked run."""
+    """``chain.VerifyBeacon`` for every stored beacon on its own stored fields: one device pass per
+    run of consecutive rounds (a whole drand.db is normally one run). Each row hashes its own
+    stored PreviousSig, so broken linkage costs nothing extra; ``linked_runs`` reports linkage."""
     engine.set_public_key(public_key)
     n = len(sb)
     ok = np.zeros(n, bool)
-    starts = linked_runs(sb)
+    starts = round_runs(sb)
     ends = np.append(starts[1:], n)
     for s, e in zip(starts.tolist(), ends.tolist()):
         plen = int(sb.prev_len[s])
-        prev0 = sb.prev[s, :plen].tobytes() if plen <= 96 else None
-        if int(sb.sig_len[s]) != 96 or prev0 is None or plen not in (32, 96):
-            # a lone malformed first beacon: kyber rejects a non-96-byte signature; an odd-length
-            # stored prev is still a well-defined message -> message-form call. A prev longer than
-            # 96 bytes is not kept by the loader and is reported as a reject (documented deviation:
-            # no drand writer produces one).
-            if prev0 is None or int(sb.sig_len[s]) != 96:
-                ok[s] = False
-                s0 = s + 1
-            else:
-                ok[s] = _verify_run(engine, int(sb.rounds[s]), prev0, [sb.sigs[s].tobytes()]) is None
-                s0 = s + 1
-            if s0 < e:
-                res = engine.verify_chained_packed(int(sb.rounds[s0]), sb.prev[s0].tobytes(),
-                                                   np.ascontiguousarray(sb.sigs[s0:e]), e - s0)
-                ok[s0:e] = res.ok
-            continue
-        res = engine.verify_chained_packed(int(sb.rounds[s]), prev0, np.ascontiguousarray(sb.sigs[s:e]), e - s)
-        ok[s:e] = res.ok
+        s0 = s
+        if plen not in (32, 96):
+            # An odd-length stored prev is still a well-defined message: message-form call for that
+            # row. A prev longer than 96 bytes is not kept by the loader and is reported as a reject
+            # (documented deviation: no drand writer produces one).
+            if plen < 96 and int(sb.sig_len[s]) == 96:
+                ok[s] = _verify_run(engine, int(sb.rounds[s]), sb.prev[s, :plen].tobytes(),
+                                    [sb.sigs[s].tobytes()]) is None
+            s0, plen = s + 1, 96
+        if s0 < e:
+            res = engine.verify_prevs(int(sb.rounds[s0]), plen, np.ascontiguousarray(sb.prev[s0:e]),
+                                      np.ascontiguousarray(sb.sigs[s0:e]), e - s0)
+            ok[s0:e] = np.asarray(res.ok, bool)
+    ok &= sb.sig_len == 96          # kyber rejects any signature that is not 96 bytes
     bad = np.flatnonzero(~ok)
     return StoreVerdict(ok, int(sb.rounds[bad[0]]) if len(bad) else None, len(starts))
 

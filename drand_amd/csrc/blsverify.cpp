@@ -361,6 +361,34 @@ int blsv_verify_chained(blsv_ctx* c, uint64_t first_round, const uint8_t* prev0,
   return BLSV_OK;
 }
 
+int blsv_verify_prevs(blsv_ctx* c, uint64_t first_round, const uint8_t* prevs96, size_t prev0_len,
+                      const uint8_t* sigs96, size_t n, uint8_t* ok_bitmap, uint64_t* first_bad,
+                      uint8_t* reject_class) {
+  if (!c) return BLSV_EINVAL;
+  if (!c->has_group) return fail(c, BLSV_ENOGROUP, "verify_prevs: no group key set");
+  if (n && (!sigs96 || !prevs96 || (prev0_len != 32 && prev0_len != 96)))
+    return fail(c, BLSV_EINVAL, "verify_prevs: row 0's prev must be 32 or 96 bytes");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, c->in_sigs.ensure(n * 96 + 96));
+  HIPCHK(c, c->seeds.ensure(n * 96 + 96));
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, sigs96, n * 96, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->seeds.p, prevs96, n * 96, hipMemcpyHostToDevice, c->stream));
+  }
+  // segments of length 1: every round hashes its own prev row (seeds[i]); row 0 uses prev0_len bytes
+  blsk::ChainedSrc src{c->in_sigs.as<uint8_t>(), c->seeds.as<uint8_t>(), first_round, 1, (uint32_t)prev0_len};
+  uint64_t fb = UINT64_MAX;
+  int rc = verify_driver(
+      c, n, c->in_sigs.as<uint8_t>(), 96, 0, group_pk(c),
+      [&](size_t base, size_t cnt) {
+        blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
+      },
+      ok_bitmap, &fb, reject_class);
+  if (rc) return rc;
+  if (first_bad) *first_bad = fb == UINT64_MAX ? UINT64_MAX : first_round + fb;
+  return BLSV_OK;
+}
+
 int blsv_verify_unchained(blsv_ctx* c, const uint64_t* rounds, uint64_t first_round, const uint8_t* sigs96, size_t n,
                           uint8_t* ok_bitmap, uint64_t* first_bad, uint8_t* reject_class) {
   if (!c) return BLSV_EINVAL;

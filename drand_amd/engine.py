@@ -44,7 +44,19 @@ def _bits(bitmap, n):
 class Engine:
     """One blsv_ctx. Not thread-safe (like the C context); create one per thread."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, init_torch: bool = True):
+        if init_torch:
+            # torch ships its own HIP runtime next to /opt/rocm's. The order bench.py uses is the
+            # one that works on the MI355X boxes: torch's runtime is up (a first allocation) before
+            # libblsverify.so is loaded, and device buffers from torch are passed to the *_dev and
+            # verify_prevs entry points.
+            try:
+                import torch
+            except ImportError:
+                torch = None
+            if torch is not None:
+                torch.cuda.set_device(int(device))
+                torch.zeros(1, device=torch.device("cuda", int(device)))
         self.lib = _lib.load()
         h = ctypes.c_void_p()
         rc = self.lib.blsv_create(int(device), ctypes.byref(h))
@@ -120,6 +132,22 @@ class Engine:
         src = (ctypes.c_uint8 * max(len(mv), 1)).from_buffer_copy(mv) if len(mv) else None
         self._check(self.lib.blsv_verify_chained(self._h, first_round, _lib.buf(prev0), len(prev0), src, n, bm,
                                                  ctypes.byref(fb), cls))
+        return BatchResult(_bits(bm, n), None if fb.value == 2 ** 64 - 1 else fb.value, list(cls)[:n])
+
+    def verify_prevs(self, first_round, prev0_len, prevs96, sigs96, n):
+        """``chain.VerifyBeacon`` for n consecutive rounds, each with its own stored PreviousSig
+        (``blsv_verify_prevs``): prevs96 / sigs96 are n*96 packed bytes (row 0's prev uses its first
+        prev0_len = 32 or 96 bytes, every other row all 96). One device pass (drand.db ranges)."""
+        p = memoryview(prevs96).cast("B")
+        q = memoryview(sigs96).cast("B")
+        if len(p) != 96 * n or len(q) != 96 * n:
+            raise ValueError("prevs and sigs must be n*96 bytes")
+        bm = _lib.out_buf((n + 7) // 8)
+        fb = ctypes.c_uint64()
+        cls = _lib.out_buf(n)
+        P = (ctypes.c_uint8 * max(len(p), 1)).from_buffer_copy(p) if n else None
+        Q = (ctypes.c_uint8 * max(len(q), 1)).from_buffer_copy(q) if n else None
+        self._check(self.lib.blsv_verify_prevs(self._h, first_round, P, prev0_len, Q, n, bm, ctypes.byref(fb), cls))
         return BatchResult(_bits(bm, n), None if fb.value == 2 ** 64 - 1 else fb.value, list(cls)[:n])
 
     def verify_unchained(self, sigs, first_round=None, rounds=None):

@@ -85,6 +85,17 @@ int blsv_verify_chained(blsv_ctx* ctx, uint64_t first_round, const uint8_t* prev
                         uint8_t* reject_class);
 
 /*
+ * chain.VerifyBeacon (chain/beacon.go:87-92) over n consecutive rounds first_round.. where each
+ * round carries its OWN PreviousSig: prevs96[i*96 ..] (row 0 uses its first prev0_len = 32 or 96
+ * bytes, every other row 96). For stored or relayed ranges whose linkage is not assumed, e.g. a
+ * drand.db read by include/boltload.h (chain/boltdb/store.go:109-128 per-round Get). Outputs as in
+ * blsv_verify_chained; first_bad is a ROUND.
+ */
+int blsv_verify_prevs(blsv_ctx* ctx, uint64_t first_round, const uint8_t* prevs96, size_t prev0_len,
+                      const uint8_t* sigs96, size_t n, uint8_t* ok_bitmap, uint64_t* first_bad,
+                      uint8_t* reject_class);
+
+/*
  * chain.VerifyBeaconV2 (chain/beacon.go:94-98): msg = sha256(BE64(round)) over SignatureV2.
  * rounds may be NULL (then round i = first_round + i).
  */

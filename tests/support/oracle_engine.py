@@ -32,6 +32,16 @@ class OracleEngine:
         b = bytes(memoryview(sigs96).cast("B"))
         return self.verify_chained(first_round, prev0, [b[96 * i:96 * (i + 1)] for i in range(n)])
 
+    def verify_prevs(self, first_round, prev0_len, prevs96, sigs96, n):
+        p, q = bytes(memoryview(prevs96).cast("B")), bytes(memoryview(sigs96).cast("B"))
+        self.calls.append(("prevs", first_round, n))
+        cls = []
+        for i in range(n):
+            prev = p[96 * i:96 * i + (prev0_len if i == 0 else 96)]
+            msg = hashlib.sha256(prev + (first_round + i).to_bytes(8, "big")).digest()
+            cls.append(self.o.verify(self.pk, msg, q[96 * i:96 * (i + 1)]))
+        return self._res(cls, first_round)
+
     def verify_unchained(self, sigs, first_round=None, rounds=None):
         rounds = rounds if rounds is not None else [first_round + i for i in range(len(sigs))]
         self.calls.append(("unchained", rounds[0], len(sigs)))

@@ -90,6 +90,7 @@ def _check_verdicts(eng, tmp_path, chain):
     write_db(p, _items(bs), per_leaf=3)
     v = boltdb.verify_store(eng, pk, boltdb.load_store(p))
     assert v.ok.all() and v.first_bad is None and v.runs == 1
+    assert boltdb.round_runs(boltdb.load_store(p)).tolist() == [0]
     tb = _tampered(bs)
     write_db(p, _items(tb), per_leaf=4)
     sb = boltdb.load_store(p)
@@ -175,3 +176,51 @@ def test_verify_store_sharded_gloo(tmp_path, chain, world):
     want = [r not in (10, 16) for r in rounds]
     for _, fb, ok in res:
         assert fb == 10 and ok == want
+
+
+def device_history_items(engine, golden, n, seg=64):
+    """A device-generated chained history (bench.py's layout) as drand.db items: rows carry the
+    PreviousSig the generator used (the segment seed at segment starts, else the previous sig)."""
+    import torch
+    g = golden["chained"]
+    dev = torch.device("cuda", 0)
+    engine.set_public_key(bytes.fromhex(g["pk"]))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(77)
+    n_seg = (n + seg - 1) // seg
+    seeds = torch.randint(0, 256, (n_seg * 96,), dtype=torch.uint8, device=dev, generator=gen)
+    sigs = torch.empty(n * 96, dtype=torch.uint8, device=dev)
+    engine.generate_chained_dev(int(g["sk"], 16).to_bytes(32, "big"), 1, seg, seeds.data_ptr(), 32, sigs.data_ptr(),
+                                n, torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    S, Q = sigs.cpu().numpy().reshape(n, 96), seeds.cpu().numpy().reshape(n_seg, 96)
+    items = []
+    for i in range(n):
+        if i % seg == 0:
+            prev = Q[i // seg, :32 if i == 0 else 96].tobytes()
+        else:
+            prev = S[i - 1].tobytes()
+        items.append((struct.pack(">Q", i + 1), ingest.beacon_to_json(Beacon(prev, i + 1, S[i].tobytes()))))
+    return items
+
+
+@pytest.mark.gpu
+def test_verify_store_gpu_scale(tmp_path, golden, engine):
+    """65,536 stored rounds (1,024 broken-linkage segments) in ONE device pass; then corruptions."""
+    n = 65536
+    items = device_history_items(engine, golden, n)
+    p = tmp_path / "big.db"
+    write_db(p, items, per_leaf=5)
+    pk = bytes.fromhex(golden["chained"]["pk"])
+    sb = boltdb.load_store(p)
+    assert len(sb) == n and len(boltdb.linked_runs(sb)) == n // 64 and boltdb.round_runs(sb).tolist() == [0]
+    v = boltdb.verify_store(engine, pk, sb)
+    assert v.ok.all() and v.first_bad is None and v.runs == 1
+    # corrupt rows in memory: a flipped bit, a cleared flag, a wrong stored prev; rows after them keep
+    # their own (unchanged) stored prev, so only the tampered rows reject
+    sb.sigs[1000, 50] ^= 1
+    sb.sigs[40000, 0] &= 0x7F
+    sb.prev[50001, 7] ^= 0x80
+    sb.sig_len[60000] = 95
+    v = boltdb.verify_store(engine, pk, sb)
+    assert np.flatnonzero(~v.ok).tolist() == [1000, 40000, 50001, 60000] and v.first_bad == 1001
