@@ -137,18 +137,23 @@ class Engine:
     def verify_prevs(self, first_round, prev0_len, prevs96, sigs96, n):
         """``chain.VerifyBeacon`` for n consecutive rounds, each with its own stored PreviousSig
         (``blsv_verify_prevs``): prevs96 / sigs96 are n*96 packed bytes (row 0's prev uses its first
-        prev0_len = 32 or 96 bytes, every other row all 96). One device pass (drand.db ranges)."""
-        p = memoryview(prevs96).cast("B")
-        q = memoryview(sigs96).cast("B")
+        prev0_len = 32 or 96 bytes, every other row all 96). One device pass (drand.db ranges).
+        Bulk form: ``ok`` and ``reject_class`` come back as numpy arrays, and the inputs are passed
+        to the library without a host copy when they are contiguous numpy arrays."""
+        import numpy as np
+        p = np.ascontiguousarray(np.frombuffer(memoryview(prevs96).cast("B"), np.uint8))
+        q = np.ascontiguousarray(np.frombuffer(memoryview(sigs96).cast("B"), np.uint8))
         if len(p) != 96 * n or len(q) != 96 * n:
             raise ValueError("prevs and sigs must be n*96 bytes")
-        bm = _lib.out_buf((n + 7) // 8)
+        bm = np.zeros(max((n + 7) // 8, 1), np.uint8)
+        cls = np.zeros(max(n, 1), np.uint8)
         fb = ctypes.c_uint64()
-        cls = _lib.out_buf(n)
-        P = (ctypes.c_uint8 * max(len(p), 1)).from_buffer_copy(p) if n else None
-        Q = (ctypes.c_uint8 * max(len(q), 1)).from_buffer_copy(q) if n else None
-        self._check(self.lib.blsv_verify_prevs(self._h, first_round, P, prev0_len, Q, n, bm, ctypes.byref(fb), cls))
-        return BatchResult(_bits(bm, n), None if fb.value == 2 ** 64 - 1 else fb.value, list(cls)[:n])
+        u8 = ctypes.POINTER(ctypes.c_uint8)
+        ptr = lambda a: a.ctypes.data_as(u8) if a.size else None
+        self._check(self.lib.blsv_verify_prevs(self._h, first_round, ptr(p), prev0_len, ptr(q), n, ptr(bm),
+                                               ctypes.byref(fb), ptr(cls)))
+        ok = np.unpackbits(bm, bitorder="little")[:n].astype(bool)
+        return BatchResult(ok, None if fb.value == 2 ** 64 - 1 else fb.value, cls[:n])
 
     def verify_unchained(self, sigs, first_round=None, rounds=None):
         n = len(sigs)

@@ -115,22 +115,50 @@ def mixed_batch(eng, g, n, seg, steps):
             "ms_per_batch": round(dt * 1e3 / steps, 3)}
 
 
+def store_check(eng, golden, n, path):
+    """§8f rank 2 end to end: a drand.db of n device-generated rounds (segments of 64, so linkage
+    breaks every 64 rounds) is loaded by libboltload and verified by blsv_verify_prevs in one pass.
+    The file is written outside the timed region (fixture creation)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from drand_amd import boltdb
+    from support.boltwriter import write_db
+    from test_boltdb import device_history_items
+    t0 = time.perf_counter()
+    write_db(path, device_history_items(eng, golden, n), per_leaf=5)
+    t_write = time.perf_counter() - t0
+    pk = bytes.fromhex(golden["chained"]["pk"])
+    boltdb.verify_store(eng, pk, boltdb.load_store(path, max_n=4096))   # warm-up
+    t0 = time.perf_counter()
+    sb = boltdb.load_store(path)
+    t_load = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    v = boltdb.verify_store(eng, pk, sb)
+    t_verify = time.perf_counter() - t0
+    assert v.ok.all() and v.runs == 1 and len(sb) == n
+    os.remove(path)
+    return {"n": n, "file_mb": None, "write_s": round(t_write, 2), "load_s": round(t_load, 3),
+            "verify_s": round(t_verify, 3), "load_threads": min(16, os.cpu_count() or 1),
+            "beacons_per_s_end_to_end": round(n / (t_load + t_verify), 1),
+            "note": "verify includes the host->device copy of prev+sig rows (192 B/beacon)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--seg-len", type=int, default=64)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--store-n", type=int, default=1_000_000, help="rounds in the drand.db leg (0 = skip)")
     args = ap.parse_args()
-    import torch
-    torch.cuda.set_device(0)   # initialise torch's HIP runtime before the engine's context (as bench.py does)
-    torch.zeros(1, device="cuda")
     from drand_amd.engine import Engine
     with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
         golden = json.load(f)
     eng = Engine(0)
     out = {"configs[2]_threshold_round": threshold_round(eng, golden["threshold"], args.reps),
            "configs[4]_mixed_batch": mixed_batch(eng, golden["chained"], args.n, args.seg_len, args.steps)}
+    if args.store_n:
+        out["configs[f2]_store_check"] = store_check(eng, golden, args.store_n, "/tmp/drand_amd_bench.db")
     print(json.dumps(out))
     eng.close()
 
