@@ -241,3 +241,29 @@ def test_segments(chain):
     segs = ingest.segments(gap)
     assert [(s.first_round, s.n, s.start) for s in segs] == [(1, 5, 0), (7, 4, 5), (11, 1, 9), (12, 13, 10)]
     assert ingest.segments([]) == []
+
+
+def scenario_wire_to_sync(eng, chain):
+    """protobuf BeaconPackets off the sync stream (protocol.proto:88-92) straight into sync_chain."""
+    pk, seed, bs = chain
+    stream = [ingest.beacon_to_packet(b) for b in bs]
+    put = []
+    out = sync_chain(eng, pk, Beacon(b"", 0, seed), (ingest.beacon_from_packet(x) for x in stream), 24, put.append,
+                     chunk=10)
+    assert out.finished and [b.round for b in put] == list(range(1, 25))
+    # an odd-length PreviousSig is still a message (sha256(prev || round)): it rejects, via the message form
+    odd = [Beacon(bs[4].previous_sig[:10], 5, bs[4].signature), bs[5]]
+    assert verify_beacons(eng, pk, odd) == [False, True]
+
+
+
+
+@pytest.mark.parametrize("scenario", [scenario_wire_to_sync], ids=lambda f: f.__name__)
+def test_wire_cpu(scenario, chain):
+    scenario(OracleEngine(), chain)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scenario", [scenario_wire_to_sync], ids=lambda f: f.__name__)
+def test_wire_gpu(scenario, chain, engine):
+    scenario(engine, chain)
