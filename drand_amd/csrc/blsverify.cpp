@@ -519,6 +519,9 @@ int blsv_verify_partials(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const 
   return BLSV_OK;
 }
 
+static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std::vector<uint32_t>& index, size_t k,
+                        size_t t, uint8_t* out_sig96);
+
 int blsv_recover(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
                  size_t k, size_t t, size_t n, uint8_t* out_sig96) {
   if (!c) return BLSV_EINVAL;
@@ -529,7 +532,13 @@ int blsv_recover(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t*
   std::vector<uint32_t> index;
   int rc = partials_stage(c, msg, msg_len, partials, partial_len, k, cls, index);
   if (rc) return rc;
-  // first t valid shares in input order, duplicate indices keep the first
+  return recover_from(c, cls, index, k, t, out_sig96);
+}
+
+// Lagrange at 0 over the first t valid shares (input order; duplicate indices keep the first) of
+// the batch partials_stage just decompressed into c->S, then the G2 MSM and compression.
+static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std::vector<uint32_t>& index, size_t k,
+                        size_t t, uint8_t* out_sig96) {
   std::vector<uint32_t> sel, idx;
   for (size_t i = 0; i < k && sel.size() < t; i++) {
     if (cls[i] != BLSV_REJ_OK) continue;
@@ -553,6 +562,35 @@ int blsv_recover(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t*
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(out_sig96, c->out.p, 96, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+int blsv_aggregate(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
+                   size_t k, size_t t, size_t n, uint8_t* ok, uint8_t* reject_class, uint8_t* out_sig96,
+                   uint8_t* group_ok) {
+  if (!c) return BLSV_EINVAL;
+  if (!out_sig96 || !ok || !group_ok || t == 0 || (k && !partials))
+    return fail(c, BLSV_EINVAL, "aggregate: bad arguments");
+  (void)n;
+  (void)hipSetDevice(c->device);
+  std::vector<uint8_t> cls;
+  std::vector<uint32_t> index;
+  int rc = partials_stage(c, msg, msg_len, partials, partial_len, k, cls, index);
+  if (rc) return rc;
+  for (size_t i = 0; i < k; i++) {
+    ok[i] = cls[i] == BLSV_REJ_OK;
+    if (reject_class) reject_class[i] = cls[i];
+  }
+  *group_ok = 0;
+  rc = recover_from(c, cls, index, k, t, out_sig96);
+  if (rc) return rc;
+  // VerifyRecovered(group key, msg, sig) (chain/beacon/chain.go:141)
+  const uint32_t len = (uint32_t)msg_len;
+  uint8_t bm = 0, cls1 = 0;
+  uint64_t fb = 0;
+  rc = blsv_verify_messages(c, nullptr, msg, &len, 1, out_sig96, &bm, &fb, &cls1);
+  if (rc) return rc;
+  *group_ok = bm & 1;
   return BLSV_OK;
 }
 

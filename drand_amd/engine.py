@@ -204,6 +204,21 @@ class Engine:
                                           _lib.buf(b"".join(bytes(p) for p in partials)), plen, k, t, n, out))
         return bytes(out)
 
+    def aggregate(self, msg, partials, t, n):
+        """One aggregator round (blsv_aggregate): (ok per partial, reject classes, group sig, group_ok)."""
+        k = len(partials)
+        plen = len(partials[0]) if k else 98
+        if any(len(p) != plen for p in partials):
+            raise ValueError("partials of one call must share a length")
+        ok = _lib.out_buf(k)
+        cls = _lib.out_buf(k)
+        out = _lib.out_buf(96)
+        gok = _lib.out_buf(1)
+        self._check(self.lib.blsv_aggregate(self._h, _lib.buf(msg), len(msg),
+                                            _lib.buf(b"".join(bytes(p) for p in partials)), plen, k, t, n, ok, cls,
+                                            out, gok))
+        return [bool(x) for x in list(ok)[:k]], list(cls)[:k], bytes(out), bool(gok[0])
+
     def sign(self, sk32, msgs, index=-1):
         n = len(msgs)
         lens = (ctypes.c_uint32 * max(n, 1))(*[len(m) for m in msgs])

@@ -96,6 +96,17 @@ int blsv_verify_prevs(blsv_ctx* ctx, uint64_t first_round, const uint8_t* prevs9
                       uint8_t* reject_class);
 
 /*
+ * One aggregator round of chain/beacon/chain.go:119-166 in two verification passes instead of three:
+ * every partial verified (tbls.VerifyPartial, node.go:112; ok / reject_class per partial), Recover
+ * over the first t valid shares in input order (chain.go:136; the shares it would re-verify got the
+ * same deterministic verdicts in this pass), then VerifyRecovered of the group signature under the
+ * group key (chain.go:141) into *group_ok. Returns BLSV_ENOTENOUGH (ok[] filled) with < t valid.
+ */
+int blsv_aggregate(blsv_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
+                   size_t k, size_t t, size_t n, uint8_t* ok, uint8_t* reject_class, uint8_t* out_sig96,
+                   uint8_t* group_ok);
+
+/*
  * chain.VerifyBeaconV2 (chain/beacon.go:94-98): msg = sha256(BE64(round)) over SignatureV2.
  * rounds may be NULL (then round i = first_round + i).
  */

@@ -87,3 +87,20 @@ def test_recover_selection_rules(engine, golden):
     with pytest.raises(EngineError) as e:
         engine.recover(msg, [bad] + partials[: t - 1], t, th["n"])
     assert e.value.code == _lib.BLSV_ENOTENOUGH
+
+
+@pytest.mark.gpu
+def test_aggregate_round(engine, golden):
+    """blsv_aggregate = VerifyPartial x k + Recover(first t valid) + VerifyRecovered (chain.go:119-166)."""
+    from drand_amd.engine import EngineError
+    th = golden["threshold"]
+    engine.set_group([bytes.fromhex(c) for c in th["commits"]], th["n"])
+    msg = bytes.fromhex(th["msg"])
+    partials = [bytes.fromhex(p) for p in th["partials"]]
+    ok, cls, sig, gok = engine.aggregate(msg, partials, th["t"], th["n"])
+    assert all(ok) and gok and sig.hex() == th["group_sig"]
+    bad = bytes.fromhex(th["bad_partial"])
+    ok, cls, sig, gok = engine.aggregate(msg, [bad] + partials[:th["t"]], th["t"], th["n"])
+    assert ok[0] is False and all(ok[1:]) and gok and sig.hex() == th["group_sig"]
+    with pytest.raises(EngineError):
+        engine.aggregate(msg, [bad] + partials[:th["t"] - 1], th["t"], th["n"])
