@@ -58,6 +58,7 @@ SIGNATURES = {
     "blsv_verify_unchained": (ctypes.c_int, [vp, u64p, ctypes.c_uint64, u8p, sz, u8p, u64p, u8p]),
     "blsv_verify_messages": (ctypes.c_int, [vp, u8p, u8p, u32p, sz, u8p, u8p, u64p, u8p]),
     "blsv_verify_partials": (ctypes.c_int, [vp, u8p, sz, u8p, sz, sz, u8p, u8p]),
+    "blsv_verify_partials_multi": (ctypes.c_int, [vp, u8p, u32p, u8p, sz, sz, u8p, u8p]),
     "blsv_recover": (ctypes.c_int, [vp, u8p, sz, u8p, sz, sz, sz, sz, u8p]),
     "blsv_aggregate": (ctypes.c_int, [vp, u8p, sz, u8p, sz, sz, sz, sz, u8p, u8p, u8p, u8p]),
     "blsv_sign": (ctypes.c_int, [vp, u8p, ctypes.c_int32, u8p, u32p, sz, u8p]),

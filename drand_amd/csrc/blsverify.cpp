@@ -452,8 +452,11 @@ int blsv_verify_messages(blsv_ctx* c, const uint8_t* pk48, const uint8_t* msgs, 
 }
 
 // shared by verify_partials / recover: returns per-partial class in cls (host), S staged on device
+// msg_lens == nullptr: every partial signs the same msg[0 .. msg_len); else partial i signs its own
+// message, msgs packed back to back with msg_lens[i] bytes each.
 static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials,
-                          size_t partial_len, size_t k, std::vector<uint8_t>& cls, std::vector<uint32_t>& index) {
+                          size_t partial_len, size_t k, std::vector<uint8_t>& cls, std::vector<uint32_t>& index,
+                          const uint32_t* msg_lens = nullptr) {
   cls.assign(k, BLSV_REJ_OK);
   index.assign(k, 0);
   if (!c->has_group) return fail(c, BLSV_ENOGROUP, "partials: no group set");
@@ -473,9 +476,13 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
   // H(msg) once per item slot (all identical); the per-item PubPoly.Eval(index) table
   std::vector<uint32_t> lens(k, (uint32_t)msg_len);
   std::vector<uint8_t> packed;
-  packed.reserve(k * msg_len);
-  for (size_t i = 0; i < k; i++) packed.insert(packed.end(), msg, msg + msg_len);
-  rc = upload_messages(c, packed.data(), lens.data(), k);
+  if (msg_lens) {
+    rc = upload_messages(c, msg, msg_lens, k);
+  } else {
+    packed.reserve(k * msg_len);
+    for (size_t i = 0; i < k; i++) packed.insert(packed.end(), msg, msg + msg_len);
+    rc = upload_messages(c, packed.data(), lens.data(), k);
+  }
   if (rc) return rc;
   blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), k,
                              c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
@@ -511,6 +518,22 @@ int blsv_verify_partials(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const 
   std::vector<uint8_t> cls;
   std::vector<uint32_t> index;
   int rc = partials_stage(c, msg, msg_len, partials, partial_len, k, cls, index);
+  if (rc) return rc;
+  for (size_t i = 0; i < k; i++) {
+    ok[i] = cls[i] == BLSV_REJ_OK;
+    if (reject_class) reject_class[i] = cls[i];
+  }
+  return BLSV_OK;
+}
+
+int blsv_verify_partials_multi(blsv_ctx* c, const uint8_t* msgs, const uint32_t* msg_lens, const uint8_t* partials,
+                               size_t partial_len, size_t k, uint8_t* ok, uint8_t* reject_class) {
+  if (!c) return BLSV_EINVAL;
+  if (k && (!partials || !ok || !msgs || !msg_lens)) return fail(c, BLSV_EINVAL, "verify_partials_multi: null arguments");
+  (void)hipSetDevice(c->device);
+  std::vector<uint8_t> cls;
+  std::vector<uint32_t> index;
+  int rc = partials_stage(c, msgs, 0, partials, partial_len, k, cls, index, msg_lens);
   if (rc) return rc;
   for (size_t i = 0; i < k; i++) {
     ok[i] = cls[i] == BLSV_REJ_OK;

@@ -196,6 +196,21 @@ class Engine:
                                                   _lib.buf(b"".join(bytes(p) for p in partials)), plen, k, ok, cls))
         return [bool(x) for x in list(ok)[:k]], list(cls)[:k]
 
+    def verify_partials_multi(self, msgs, partials):
+        """Partials of many rounds in one pass: partial i signs msgs[i] (blsv_verify_partials_multi)."""
+        k = len(partials)
+        assert len(msgs) == k
+        plen = len(partials[0]) if k else 98
+        if any(len(p) != plen for p in partials):
+            raise ValueError("partials of one call must share a length")
+        lens = (ctypes.c_uint32 * max(k, 1))(*[len(m) for m in msgs])
+        ok = _lib.out_buf(k)
+        cls = _lib.out_buf(k)
+        self._check(self.lib.blsv_verify_partials_multi(self._h, _lib.buf(b"".join(bytes(m) for m in msgs)), lens,
+                                                        _lib.buf(b"".join(bytes(p) for p in partials)), plen, k, ok,
+                                                        cls))
+        return [bool(x) for x in list(ok)[:k]], list(cls)[:k]
+
     def recover(self, msg, partials, t, n):
         k = len(partials)
         plen = len(partials[0]) if k else 98

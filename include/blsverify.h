@@ -107,6 +107,15 @@ int blsv_aggregate(blsv_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint
                    uint8_t* group_ok);
 
 /*
+ * tbls.VerifyPartial (chain/beacon/node.go:112,125) over partials of MANY rounds in one pass:
+ * partial i signs msgs[off_i .. off_i + msg_lens[i]) (messages packed back to back), e.g. a catch-up
+ * of cached partials across rounds (chain/beacon/cache.go:112-182). Same outputs as
+ * blsv_verify_partials. At most the context's chunk capacity of partials per call.
+ */
+int blsv_verify_partials_multi(blsv_ctx* ctx, const uint8_t* msgs, const uint32_t* msg_lens, const uint8_t* partials,
+                               size_t partial_len, size_t k, uint8_t* ok, uint8_t* reject_class);
+
+/*
  * chain.VerifyBeaconV2 (chain/beacon.go:94-98): msg = sha256(BE64(round)) over SignatureV2.
  * rounds may be NULL (then round i = first_round + i).
  */

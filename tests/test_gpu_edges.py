@@ -104,3 +104,24 @@ def test_aggregate_round(engine, golden):
     assert ok[0] is False and all(ok[1:]) and gok and sig.hex() == th["group_sig"]
     with pytest.raises(EngineError):
         engine.aggregate(msg, [bad] + partials[:th["t"] - 1], th["t"], th["n"])
+
+
+@pytest.mark.gpu
+def test_verify_partials_multi_rounds(engine, golden):
+    """Partials of 24 different rounds in one pass. Group = the single golden key (t = 1, share index
+    0, as mock/result.go:88-95 signs with PriShare{I: 0}); partial_i = BE16(0) || sig_i over
+    Message(round_i, prev_i)."""
+    import hashlib
+    ch = golden["chained"]
+    engine.set_group([bytes.fromhex(ch["pk"])], 1)
+    msgs = [hashlib.sha256(bytes.fromhex(b["prev"]) + b["round"].to_bytes(8, "big")).digest() for b in ch["beacons"]]
+    parts = [b"\0\0" + bytes.fromhex(b["sig"]) for b in ch["beacons"]]
+    ok, cls = engine.verify_partials_multi(msgs, parts)
+    assert all(ok) and set(cls) == {0}
+    swapped = msgs[:]
+    swapped[3], swapped[17] = swapped[17], swapped[3]
+    ok, cls = engine.verify_partials_multi(swapped, parts)
+    assert [i for i, v in enumerate(ok) if not v] == [3, 17] and cls[3] == O.REJ_PAIRING
+    # agrees with the single-message entry point round by round
+    for i in (0, 9, 23):
+        assert engine.verify_partials(msgs[i], [parts[i]])[0] == [True]
