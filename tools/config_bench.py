@@ -153,12 +153,31 @@ def store_check(eng, golden, n, path):
             "note": "verify includes the host->device copy of prev+sig rows (192 B/beacon)"}
 
 
+def partials_many_rounds(eng, golden, n):
+    """Partials of n different rounds in one blsv_verify_partials_multi pass (t = 1 group of the
+    golden key; partials signed on device by blsv_sign with share index 0)."""
+    import hashlib
+    g = golden["chained"]
+    sk32 = int(g["sk"], 16).to_bytes(32, "big")
+    eng.set_group([bytes.fromhex(g["pk"])], 1)
+    msgs = [hashlib.sha256(r.to_bytes(8, "big")).digest() for r in range(1, n + 1)]
+    parts = eng.sign(sk32, msgs, index=0)
+    ok, _ = eng.verify_partials_multi(msgs[:1024], parts[:1024])   # warm-up
+    t0 = time.perf_counter()
+    ok, _ = eng.verify_partials_multi(msgs, parts)
+    dt = time.perf_counter() - t0
+    assert all(ok)
+    return {"n": n, "partials_per_s": round(n / dt, 1), "s": round(dt, 3),
+            "note": "host-buffer entry point: includes staging copies and ctypes packing"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--seg-len", type=int, default=64)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--partials-n", type=int, default=262144, help="partials in the many-rounds leg (0 = skip)")
     ap.add_argument("--store-n", type=int, default=1_000_000, help="rounds in the drand.db leg (0 = skip)")
     args = ap.parse_args()
     from drand_amd.engine import Engine
@@ -167,6 +186,8 @@ def main():
     eng = Engine(0)
     out = {"configs[2]_threshold_round": threshold_round(eng, golden["threshold"], args.reps),
            "configs[4]_mixed_batch": mixed_batch(eng, golden["chained"], args.n, args.seg_len, args.steps)}
+    if args.partials_n:
+        out["configs[2]_partials_many_rounds"] = partials_many_rounds(eng, golden, args.partials_n)
     if args.store_n:
         out["configs[f2]_store_check"] = store_check(eng, golden, args.store_n, "/tmp/drand_amd_bench.db")
     print(json.dumps(out))
