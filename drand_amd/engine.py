@@ -38,7 +38,10 @@ class BatchResult:
 
 
 def _bits(bitmap, n):
-    return [bool(bitmap[i // 8] >> (i % 8) & 1) for i in range(n)]
+    import numpy as np
+    if n == 0:
+        return []
+    return np.unpackbits(np.frombuffer(bytes(bitmap), np.uint8), bitorder="little")[:n].astype(bool).tolist()
 
 
 class Engine:
