@@ -1,19 +1,32 @@
 """Benchmark: drand chained-beacon batch verification (chain.VerifyBeacon semantics) on MI355X.
 
 Metric (BASELINE.json): beacons verified/s (batch chain verify) at 1/2/4/8 MI355X vs host-CPU.
-Workload at N=1 = BASELINE.json configs[1]: a 1,000,000-round synthetic chained beacon history
-verified on one MI355X, one pairing-product check per round. Per rank the history is generated on
-the device (client/test/result/mock/result.go:98-132 recipe: single key, seeded prev) as
-independently seeded chained segments of --seg-len rounds (a continuous 1M chain is
-inherently sequential to SIGN; verification work per round is identical either way).
+
+Default workload at N=1 = BASELINE.json configs[1]: a 1,000,000-round synthetic chained beacon
+history verified on one MI355X, one pairing-product check per round. Per rank the history is
+generated on the device (client/test/result/mock/result.go:98-132 recipe: single key, seeded prev)
+as independently seeded chained segments of --seg-len rounds (a continuous 1M chain
+is inherently sequential to SIGN; verification work per round is identical either way). With N>1
+each rank verifies its own --n rounds (weak scaling).
+
+--total-rounds T = configs[3] (strong scaling): ONE T-round history (same segment layout, segment
+seeds drawn from one fixed generator, identical on every rank) split into contiguous shard ranges
+(drand_amd/shard.py shard_range, NOT 64-aligned in general). Each rank generates its range plus the
+head of the segment it starts in, so the halo it hands the verifier as seeds[0] (seg_phase) is the
+true previous signature of its first round. --slice R/W runs rank R of a W-way split in a single
+process (the 12.5M-round slice of configs[3] on one GPU).
 
 One step = one blsv_verify_chained_dev call over the rank's whole HBM-resident shard (hash-to-G2,
 decompress + subgroup, 2-pair Miller loop, final exponentiation, verdict bitmap + first bad round),
-followed for N>1 by the north_star's exchange: an all-reduce MIN of first_bad and an all-gather of
-the per-shard verdict bitmaps over RCCL. Weak scaling: each rank verifies its own --n rounds of a
-contiguous round range.
+followed for N>1 by the exchange: an all-reduce MIN of first_bad and an all-gather of the per-shard
+verdict bitmaps over RCCL (re-packed to global bit positions on the device for unaligned shards).
+
+Correctness gate before timing: every round verifies, then a negative control -- one signature per
+rank corrupted (bit flip in x) must make exactly that round and the next one reject, with first_bad
+= the lowest corrupted round over all ranks.
 
 Usage: python bench.py [--gpus N --steps K --warmup W --n BEACONS_PER_GPU]
+       python bench.py --total-rounds 100000000 --slice 7/8
        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 """
 from __future__ import annotations
@@ -68,11 +81,15 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=1_000_000, help="beacons per GPU (configs[1]: 1M)")
+    ap.add_argument("--total-rounds", type=int, default=0,
+                    help="strong scaling (configs[3]): one history of this many rounds split over the ranks")
+    ap.add_argument("--slice", default="", help="R/W: verify shard R of a W-way split in this one process")
     ap.add_argument("--seg-len", type=int, default=64, help="rounds per independently seeded chained segment")
     ap.add_argument("--cpu-per-worker", type=int, default=384, help="C-oracle beacons per host thread (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=16)
     args = ap.parse_args()
 
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -94,16 +111,42 @@ def main():
     sk32 = int(g["sk"], 16).to_bytes(32, "big")
     pk48 = bytes.fromhex(g["pk"])
     opc = load_json("profiles/opcount.json")["fp_mul"]
-
-    n = args.n
     seg = args.seg_len
-    n_seg = (n + seg - 1) // seg
-    first_round = rank * n + 1  # contiguous round range per rank
-    seed0_len = 32 if rank == 0 else 96  # round 1 hashes the 32-byte genesis seed (client/verify.go:122)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(0xD7A4D + rank)
-    seeds = torch.randint(0, 256, (n_seg * 96,), dtype=torch.uint8, device=dev, generator=gen)
-    sigs = torch.empty(n * 96, dtype=torch.uint8, device=dev)
+
+    strong = args.total_rounds > 0
+    if args.slice:
+        s_rank, s_world = (int(x) for x in args.slice.split("/"))
+        assert world == 1 and strong and 0 <= s_rank < s_world, "--slice R/W needs --total-rounds and one process"
+    else:
+        s_rank, s_world = rank, world
+    if strong:
+        sl = shard.segmented_slice(args.total_rounds, s_world, s_rank, seg)
+        counts = [shard.shard_range(args.total_rounds, s_world, r).count for r in range(s_world)]
+        n = sl.shard.count
+        first_round = sl.shard.first_round
+        gen_first_round = sl.gen_start + 1
+        # every rank draws the SAME global seed table and keeps its segments' rows
+        n_seg_total = (args.total_rounds + seg - 1) // seg
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(0xD7A4D)
+        all_seeds = torch.randint(0, 256, (n_seg_total, 96), dtype=torch.uint8, device=dev, generator=gen)
+        gen_seeds = all_seeds[sl.seg_first:sl.seg_first + sl.n_seg].contiguous()
+        del all_seeds
+        gen_seed0_len = 32 if sl.seg_first == 0 else 96
+        gen_n = sl.gen_count
+        phase = sl.phase
+    else:
+        n = args.n
+        counts = [n] * world
+        first_round = gen_first_round = rank * n + 1  # contiguous round range per rank
+        gen_seed0_len = 32 if rank == 0 else 96  # round 1 hashes the 32-byte genesis seed (client/verify.go:122)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(0xD7A4D + rank)
+        gen_seeds = torch.randint(0, 256, ((n + seg - 1) // seg, 96), dtype=torch.uint8, device=dev, generator=gen)
+        gen_n = n
+        phase = 0
+    seed0_len = 32 if first_round == 1 else 96
+    gen_sigs = torch.empty((max(gen_n, 1), 96), dtype=torch.uint8, device=dev)
     words = (n + 63) // 64
     bitmap = torch.zeros(words, dtype=torch.int64, device=dev)
     first_bad = torch.empty(1, dtype=torch.int64, device=dev)
@@ -113,28 +156,59 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     t_gen = time.perf_counter()
-    eng.generate_chained_dev(sk32, first_round, seg, seeds.data_ptr(), seed0_len, sigs.data_ptr(), n, sp)
+    eng.generate_chained_dev(sk32, gen_first_round, seg, gen_seeds.data_ptr(), gen_seed0_len, gen_sigs.data_ptr(),
+                             gen_n, sp)
     torch.cuda.synchronize(dev)
     t_gen = time.perf_counter() - t_gen
+    sigs = gen_sigs[phase:phase + n]  # the rank's shard (phase = 0 in weak mode)
+    seeds = shard.local_seeds(sl, gen_seeds, gen_sigs) if strong else gen_seeds
 
     def step():
         eng.verify_chained_dev(first_round, seg, seeds.data_ptr(), seed0_len, sigs.data_ptr(), n,
-                               bitmap.data_ptr(), first_bad.data_ptr(), None, sp)
+                               bitmap.data_ptr(), first_bad.data_ptr(), None, sp, seg_phase=phase)
         if world > 1:
             # per-shard first bad ROUND -> global min; per-shard bitmaps -> every rank (RCCL over xGMI)
-            return shard.combine(first_bad, bitmap, n, to_host=False)
+            return shard.combine(first_bad, bitmap, n, to_host=False, counts=counts)
         return first_bad, bitmap
+
+    def verdicts():
+        fb, bm = step()
+        torch.cuda.synchronize(dev)
+        total = sum(counts) if world > 1 else n
+        ok = np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little")[:total].astype(bool)
+        fbv = int(fb.item()) & (2 ** 64 - 1)
+        return (None if fbv in (2 ** 64 - 1, shard.NONE_I64) else fbv), ok
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    # correctness gate: every generated round must verify
-    fb, bm = step()
-    torch.cuda.synchronize(dev)
-    ones = int(sum(bin(int(x) & (2 ** 64 - 1)).count("1") for x in bm.cpu().tolist()))
-    fbv = int(fb.item()) & (2 ** 64 - 1)
-    assert fbv in (2 ** 64 - 1, shard.NONE_I64) and ones == n * world, \
-        f"verification failed: first_bad={fbv} ones={ones}"
+    # correctness gate 1: every generated round verifies
+    fbv, ok = verdicts()
+    assert fbv is None and ok.all(), f"verification failed: first_bad={fbv} rejected={int((~ok).sum())}"
+    # gate 2 (negative control): one corrupted signature per rank -> exactly it and its successor reject
+    def bad_index(count, ph):  # a round whose successor is in the same segment (its prev = the bad sig)
+        b = count // 2
+        return b - 1 if b > 0 and (b + 1 + ph) % seg == 0 else b
+
+    if strong:
+        phases = [shard.segmented_slice(args.total_rounds, s_world, r, seg).phase for r in range(s_world)]
+    else:
+        phases = [0] * world
+    bad_i = bad_index(n, phase)
+    saved = sigs[bad_i].clone()
+    sigs[bad_i, 50] ^= 1  # bit flip in x.c0
+    fbv, ok = verdicts()
+    sigs[bad_i].copy_(saved)
+    gate = list(zip(counts, phases)) if world > 1 else [(n, phase)]
+    want = np.ones(len(ok), bool)
+    for r, (c, ph) in enumerate(gate):
+        off, b = sum(x[0] for x in gate[:r]), bad_index(c, ph)
+        want[off + b] = False
+        if b + 1 < c:
+            want[off + b + 1] = False
+    want_fb = (first_round - (sum(counts[:rank]) if world > 1 else 0)) + bad_index(*gate[0])
+    assert (ok == want).all() and fbv == want_fb, f"negative control failed: first_bad={fbv} want {want_fb} " \
+        f"rejected={np.flatnonzero(~ok)[:8].tolist()}"
 
     eng.profile(True)
     eng.profile_read()
@@ -155,7 +229,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    total = n * world * args.steps
+    total = (sum(counts) if world > 1 else n) * args.steps
     value = total / dt
     ms_per_step = dt * 1e3 / args.steps
 
@@ -179,6 +253,16 @@ def main():
         traffic = None
     per_beacon_fp_mul = sum(opc.values())
 
+    if strong:
+        workload = {"workload": "configs[3]: one %d-round chained history split in %d contiguous range shards%s, "
+                                "chain.VerifyBeacon per round, true previous-signature halo per shard"
+                                % (args.total_rounds, s_world, " (this process: shard %d, rounds %d..%d)"
+                                   % (s_rank, first_round, first_round + n - 1) if args.slice else ""),
+                    "total_rounds": args.total_rounds, "shard_rounds": n, "segment_len": seg, "seg_phase": phase,
+                    "parallelism": "range-shard x%d" % s_world}
+    else:
+        workload = {"workload": "configs[1]: %d-round chained beacon history per GPU, chain.VerifyBeacon per round"
+                                % n, "beacons_per_gpu": n, "segment_len": seg, "parallelism": "range-shard x%d" % world}
     out = {
         "metric": "beacons verified/s (batch chain verify)",
         "value": round(value, 1),
@@ -188,12 +272,11 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u32 (381-bit Montgomery, 12x32-bit limbs)",
         "data": "synthetic (device-generated chained beacons, seeded key = golden fixture key)",
-        "config": {"workload": "configs[1]: %d-round chained beacon history per GPU, chain.VerifyBeacon per round"
-                               % n, "beacons_per_gpu": n, "segment_len": seg, "parallelism": "range-shard x%d" % world},
+        "config": workload,
         "roofline": {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak, 3),
                      "unit": "T limb-products/s (v_mad_u64_u32)", "frac": round(achieved / peak, 4),
                      "traffic": traffic,
@@ -203,14 +286,16 @@ def main():
                                                   / (peak * 1e12), 4)},
         "stages_ms_per_launch": {s: round(v["ms_per_launch"], 3) for s, v in stages.items()},
         "generate_s": round(t_gen, 2),
+        "gate": "all rounds accept; negative control (one bit-flipped signature per rank) rejects exactly it and "
+                "the next round, first_bad = lowest corrupted round",
     }
-    if rank == 0 and world == 1 and args.cpu_per_worker > 0:  # CPU baseline: rank 0 at N=1 only
+    if rank == 0 and world == 1 and args.cpu_per_worker > 0 and not strong:  # CPU baseline: rank 0 at N=1 only
         # bounded sample of the same workload: the first whole segments of the rank-0 shard
         workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
-        n_seg_cpu = min(n_seg, max(1, (workers * args.cpu_per_worker + seg - 1) // seg))
+        n_seg_cpu = min(len(seeds), max(1, (workers * args.cpu_per_worker + seg - 1) // seg))
         m = min(n, n_seg_cpu * seg)
-        sh = sigs[: m * 96].cpu().numpy().tobytes()
-        sd = seeds[: n_seg_cpu * 96].cpu().numpy().tobytes()
+        sh = sigs[:m].cpu().numpy().tobytes()
+        sd = seeds[:n_seg_cpu].cpu().numpy().tobytes()
         segments = []
         for s_i in range(n_seg_cpu):
             lo, hi = s_i * seg, min(m, (s_i + 1) * seg)

@@ -17,6 +17,12 @@ BLSV_EHIP = -2
 BLSV_ENOGROUP = -3
 BLSV_ENOTENOUGH = -4
 
+AGG_OK = 0
+AGG_OK_V2 = 1
+AGG_V1_RECOVER_FAIL = 2
+AGG_V1_INVALID = 3
+AGG_V2_RECOVER_FAIL = 4
+
 REJ_OK = 0
 REJ_LENGTH = 1
 REJ_FLAG = 2
@@ -61,8 +67,11 @@ SIGNATURES = {
     "blsv_verify_partials_multi": (ctypes.c_int, [vp, u8p, u32p, u8p, sz, sz, u8p, u8p]),
     "blsv_recover": (ctypes.c_int, [vp, u8p, sz, u8p, sz, sz, sz, sz, u8p]),
     "blsv_aggregate": (ctypes.c_int, [vp, u8p, sz, u8p, sz, sz, sz, sz, u8p, u8p, u8p, u8p]),
+    "blsv_aggregate_round": (ctypes.c_int, [vp, u8p, sz, u8p, sz, u8p, sz, u8p, sz, sz, sz, sz, u8p, u8p, u8p, u8p,
+                                             ctypes.POINTER(ctypes.c_int32), u8p]),
     "blsv_sign": (ctypes.c_int, [vp, u8p, ctypes.c_int32, u8p, u32p, sz, u8p]),
-    "blsv_verify_chained_dev": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, vp, sz, vp, sz, vp, vp, vp, vp]),
+    "blsv_verify_chained_dev": (ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, vp, sz, vp, sz,
+                                                vp, vp, vp, vp]),
     "blsv_generate_chained_dev": (ctypes.c_int, [vp, u8p, ctypes.c_uint64, ctypes.c_uint64, vp, sz, vp, sz, vp]),
     "blsv_profile_enable": (ctypes.c_int, [vp, ctypes.c_int]),
     "blsv_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p, u64p, ctypes.c_int]),

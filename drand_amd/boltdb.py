@@ -123,16 +123,28 @@ def round_runs(sb: StoredBeacons):
     return np.flatnonzero(~cont)
 
 
-def verify_store(engine, public_key: bytes, sb: StoredBeacons) -> StoreVerdict:
+def verify_store(engine, public_key: bytes, sb: StoredBeacons, group_hash: bytes | None = None) -> StoreVerdict:
     """``chain.VerifyBeacon`` for every stored beacon on its own stored fields: one device pass per
     run of consecutive rounds (a whole drand.db is normally one run). Each row hashes its own
-    stored PreviousSig, so broken linkage costs nothing extra; ``linked_runs`` reports linkage."""
+    stored PreviousSig, so broken linkage costs nothing extra; ``linked_runs`` reports linkage.
+
+    Round 0 is the genesis beacon every node stores at startup (chain/beacon/node.go:69,
+    core/drand_control.go:838: ``Put(chain.GenesisBeacon(info))``): no PreviousSig and a 32-byte
+    Signature = GroupHash (chain/store.go:234-238). The reference never verifies it (sync starts at
+    last+1, sync.go:91; the client walk starts at round 1, client/verify.go:122), so it is the
+    trusted root here too: never handed to the engine and never a ``first_bad``. With
+    ``group_hash`` given, its ok bit says whether the stored Signature equals it."""
     engine.set_public_key(public_key)
     n = len(sb)
     ok = np.zeros(n, bool)
+    genesis = sb.rounds == 0
     starts = round_runs(sb)
     ends = np.append(starts[1:], n)
     for s, e in zip(starts.tolist(), ends.tolist()):
+        if genesis[s]:  # a genesis row always ends its run: the next row's prev is 32 bytes
+            s += 1
+            if s >= e:
+                continue
         plen = int(sb.prev_len[s])
         s0 = s
         if plen not in (32, 96):
@@ -148,7 +160,14 @@ def verify_store(engine, public_key: bytes, sb: StoredBeacons) -> StoreVerdict:
                                       np.ascontiguousarray(sb.sigs[s0:e]), e - s0)
             ok[s0:e] = np.asarray(res.ok, bool)
     ok &= sb.sig_len == 96          # kyber rejects any signature that is not 96 bytes
-    bad = np.flatnonzero(~ok)
+    if genesis.any():
+        gi = np.flatnonzero(genesis)
+        if group_hash is None:
+            ok[gi] = True
+        else:
+            gh = bytes(group_hash)
+            ok[gi] = [int(sb.sig_len[i]) == len(gh) and sb.sigs[i, :len(gh)].tobytes() == gh for i in gi]
+    bad = np.flatnonzero(~ok & ~genesis)
     return StoreVerdict(ok, int(sb.rounds[bad[0]]) if len(bad) else None, len(starts))
 
 
@@ -173,7 +192,7 @@ def _words(ok: np.ndarray) -> np.ndarray:
     return np.packbits(padded, bitorder="little").view(np.int64)
 
 
-def verify_store_sharded(engine, public_key: bytes, path, device=None, group=None):
+def verify_store_sharded(engine, public_key: bytes, path, device=None, group=None, group_hash=None):
     """Multi-GPU offline check of one store (SURVEY.md §8e applied to §8f rank 2).
 
     Each rank loads and verifies a contiguous slice of the stored entries (``shard.shard_range``).
@@ -188,7 +207,7 @@ def verify_store_sharded(engine, public_key: bytes, path, device=None, group=Non
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     sh = shard.shard_range(store_count(path), world, rank)
     sb = load_store(path, start=sh.start, max_n=sh.count)
-    v = verify_store(engine, public_key, sb)
+    v = verify_store(engine, public_key, sb, group_hash)
     words = torch.from_numpy(_words(v.ok).copy())
     if device is not None:
         words = words.to(device)

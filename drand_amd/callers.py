@@ -268,3 +268,200 @@ def verify_beacons(engine, public_key: bytes, beacons) -> list:
         res = engine.verify_chained(seg.first_round, seg.prev0, seg.sigs)
         ok[seg.start:seg.start + seg.n] = res.ok
     return ok
+
+
+# --------------------------------------------------------------------------------------------------
+# Threshold aggregation: chainStore.runAggregator (chain/beacon/chain.go:91-190)
+# and its partialCache / roundCache (chain/beacon/cache.go:18-182), restated. The cache, the gate and
+# the flush rules are host bookkeeping, as in the reference; the aggregation step itself (verify every
+# cached V1 and V2 partial, Recover both, VerifyRecovered both) is ONE engine call,
+# ``Engine.aggregate_round`` -> blsv_aggregate_round: two device passes for the whole round.
+
+MAX_PARTIALS_PER_NODE = 100     # chain/beacon/constants.go:14
+PARTIAL_CACHE_STORE_LIMIT = 3   # chain/beacon/chain.go:87
+
+AGG_OK, AGG_OK_V2, AGG_V1_RECOVER_FAIL, AGG_V1_INVALID, AGG_V2_RECOVER_FAIL = range(5)  # include/blsverify.h
+
+
+@dataclass
+class PartialBeaconPacket:
+    """``drand.PartialBeaconPacket`` (protobuf/drand/protocol.proto:62-72)."""
+    round: int
+    previous_sig: bytes
+    partial_sig: bytes
+    partial_sig_v2: bytes = b""
+
+
+def index_of(partial: bytes) -> int:
+    """``key.Scheme.IndexOf`` ([ext] tbls): the 2-byte big-endian share index; -1 on a short share
+    (the callers ignore the error, cache.go:42,91,133)."""
+    return int.from_bytes(bytes(partial[:2]), "big") if len(partial) >= 2 else -1
+
+
+def message(round_: int, prev: bytes) -> bytes:
+    """``chain.Message`` (chain/beacon.go:103-108)."""
+    return hashlib.sha256(bytes(prev) + round_.to_bytes(8, "big")).digest()
+
+
+def message_v2(round_: int) -> bytes:
+    """``chain.MessageV2`` (chain/beacon.go:110-114)."""
+    return hashlib.sha256(round_.to_bytes(8, "big")).digest()
+
+
+class RoundCache:
+    """``roundCache`` (cache.go:112-182): the partials of one (round, prev) keyed by share index."""
+
+    def __init__(self, id_: bytes, p: PartialBeaconPacket):
+        self.round = p.round
+        self.prev = bytes(p.previous_sig)
+        self.id = id_
+        self.sigs: dict = {}
+        self.sigs_v2: dict = {}
+
+    def append(self, p: PartialBeaconPacket) -> bool:
+        idx = index_of(p.partial_sig)
+        if idx in self.sigs:
+            return False
+        self.sigs[idx] = bytes(p.partial_sig)
+        if len(p.partial_sig_v2) > 0:  # a V2 partial missing the first time is never added later
+            self.sigs_v2[idx] = bytes(p.partial_sig_v2)
+        return True
+
+    def __len__(self):
+        return len(self.sigs)
+
+    def len_v2(self):
+        return len(self.sigs_v2)
+
+    def msg(self):
+        return message(self.round, self.prev)
+
+    def partials(self):
+        return list(self.sigs.values())
+
+    def partials_v2(self):
+        return list(self.sigs_v2.values())
+
+    def flush_index(self, idx):
+        self.sigs.pop(idx, None)
+
+
+def round_id(round_: int, prev: bytes) -> bytes:
+    """cache.go:33-38: BE64(round) || previous."""
+    return round_.to_bytes(8, "big") + bytes(prev)
+
+
+class PartialCache:
+    """``partialCache`` (cache.go:18-110): per-round caches plus the per-signer round list that
+    bounds a signer to MAX_PARTIALS_PER_NODE cached rounds (the oldest is evicted)."""
+
+    def __init__(self, log=None):
+        self.rounds: dict = {}
+        self.rcvd: dict = {}
+        self.log = log or (lambda *a: None)
+
+    def append(self, p: PartialBeaconPacket):
+        id_ = round_id(p.round, p.previous_sig)
+        idx = index_of(p.partial_sig)
+        rc = self._get_cache(id_, p)
+        if rc is None:
+            return
+        if rc.append(p):
+            self.rcvd.setdefault(idx, []).append(id_)
+
+    def flush_rounds(self, round_: int):
+        for id_, rc in list(self.rounds.items()):
+            if rc.round > round_:
+                continue
+            del self.rounds[id_]
+            for idx in list(rc.sigs):
+                keep = [x for x in self.rcvd.get(idx, []) if x != id_]
+                if keep:
+                    self.rcvd[idx] = keep
+                else:
+                    self.rcvd.pop(idx, None)
+
+    def get_round_cache(self, round_: int, prev: bytes):
+        return self.rounds.get(round_id(round_, prev))
+
+    def _get_cache(self, id_, p):
+        if id_ in self.rounds:
+            return self.rounds[id_]
+        idx = index_of(p.partial_sig)
+        if len(self.rcvd.get(idx, [])) >= MAX_PARTIALS_PER_NODE:
+            to_evict = self.rcvd[idx][0]
+            rc = self.rounds.get(to_evict)
+            if rc is None:
+                self.log("cache miss", idx, p.round)
+                return None
+            rc.flush_index(idx)
+            self.rcvd[idx] = self.rcvd[idx][1:] + [id_]
+            if len(rc) == 0:
+                del self.rounds[to_evict]
+        rc = RoundCache(id_, p)
+        self.rounds[id_] = rc
+        return rc
+
+
+@dataclass
+class AggregateEvent:
+    """What one partial did to the aggregator (the reference only logs these)."""
+    kind: str                       # "ignored", "stored", "invalid_recovery", "invalid_sig",
+                                    # "invalid_recovery_v2", "aggregated"
+    round: int
+    beacon: Optional[Beacon] = None
+    appended: bool = False          # tryAppend succeeded (chain.go:192-208)
+    v2_valid: Optional[bool] = None  # VerifyRecovered V2 (a failure only logs, chain.go:162-164)
+
+
+class Aggregator:
+    """``chainStore.runAggregator`` (chain/beacon/chain.go:91-190) over one GPU engine.
+
+    ``on_partial`` is the ``newPartials`` case (partials already passed ``ProcessPartialBeacon``'s
+    VerifyPartial, node.go:112); ``on_beacon_stored`` the ``beaconStoredAgg`` case. ``put`` stands for
+    ``CallbackStore.Put`` (raises on a rejected beacon). ``commits``/``t``/``n`` are the current
+    group's (``c.crypto.GetPub()``, ``GetGroup().Threshold``/``Len()``); ``set_group`` follows a
+    reshare transition (node.go:190)."""
+
+    def __init__(self, engine, commits, t: int, n: int, last: Beacon, put: Callable[[Beacon], None]):
+        self.engine = engine
+        self.put = put
+        self.last = last
+        self.cache = PartialCache()
+        self.set_group(commits, t, n)
+
+    def set_group(self, commits, t, n):
+        self.commits, self.t, self.n = [bytes(c) for c in commits], int(t), int(n)
+
+    def on_beacon_stored(self, b: Beacon):
+        self.last = b
+        self.cache.flush_rounds(b.round)
+
+    def on_partial(self, p: PartialBeaconPacket) -> AggregateEvent:
+        r = p.round
+        if not (self.last.round < r <= self.last.round + PARTIAL_CACHE_STORE_LIMIT + 1):
+            return AggregateEvent("ignored", r)
+        self.cache.append(p)
+        rc = self.cache.get_round_cache(r, p.previous_sig)
+        if rc is None or len(rc) < self.t:
+            return AggregateEvent("stored", r)
+        self.engine.set_group(self.commits, self.n)
+        status, _, _, sig1, sig2, v2_valid = self.engine.aggregate_round(
+            rc.msg(), rc.partials(), message_v2(r), rc.partials_v2(), self.t, self.n)
+        if status == AGG_V1_RECOVER_FAIL:
+            return AggregateEvent("invalid_recovery", r)
+        if status == AGG_V1_INVALID:
+            return AggregateEvent("invalid_sig", r)
+        if status == AGG_V2_RECOVER_FAIL:
+            return AggregateEvent("invalid_recovery_v2", r)
+        b = Beacon(rc.prev, rc.round, sig1, sig2 if status == AGG_OK_V2 else b"")
+        self.cache.flush_rounds(r)
+        ev = AggregateEvent("aggregated", r, b, v2_valid=v2_valid if status == AGG_OK_V2 else None)
+        if self.last.round + 1 == b.round:  # tryAppend (chain.go:192-208)
+            try:
+                self.put(b)
+                ev.appended = True
+                self.last = b
+            except Exception:  # noqa: BLE001 - chain.go:197-200 logs and returns false
+                pass
+        return ev

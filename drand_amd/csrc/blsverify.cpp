@@ -64,6 +64,10 @@ struct blsv_ctx {
   bool has_group = false;
   size_t t = 0, n = 0;
   DBuf commits, commit_inf;
+  std::vector<uint8_t> group_bytes;  // the commitments of the current group (set_group is a no-op on a repeat)
+  // PubPoly.Eval(i) for every share index i < min(n, 65536), computed once per group
+  DBuf pk_all, pk_all_inf;
+  size_t pk_all_n = 0;
   // explicit-pk override (verify_messages with pk48)
   DBuf pk_tab, pk_inf;
   uint8_t pk_cache[48];
@@ -319,16 +323,38 @@ int blsv_synchronize(blsv_ctx* c) {
 int blsv_set_group(blsv_ctx* c, const uint8_t* commits48, size_t t, size_t n) {
   if (!c || !commits48 || t == 0 || t > 65536) return fail(c, BLSV_EINVAL, "set_group: bad arguments");
   (void)hipSetDevice(c->device);
+  // the same group again (every caller sets its key per call): nothing to decode or evaluate
+  if (c->has_group && c->t == t && c->n == n && c->group_bytes.size() == t * 48 &&
+      memcmp(c->group_bytes.data(), commits48, t * 48) == 0)
+    return BLSV_OK;
+  c->has_group = false;
+  c->group_bytes.clear();
   std::vector<uint8_t> cls;
   int rc = decode_g1(c, commits48, t, c->commits, c->commit_inf, cls);
   if (rc) return rc;
   for (size_t i = 0; i < t; i++)
-    if (cls[i]) {
-      c->has_group = false;
-      return fail(c, BLSV_EINVAL, "set_group: commitment %zu rejected (class %d)", i, (int)cls[i]);
-    }
+    if (cls[i]) return fail(c, BLSV_EINVAL, "set_group: commitment %zu rejected (class %d)", i, (int)cls[i]);
+  // PK_i = PubPoly.Eval(i) for every member index (key/keys.go:239-241; share x = i + 1): the partial
+  // verifications index this table instead of re-running Horner per partial and call
+  const size_t m = std::min<size_t>(n, 65536);
+  c->pk_all_n = 0;
+  if (m) {
+    std::vector<uint32_t> ident(m);
+    for (size_t i = 0; i < m; i++) ident[i] = (uint32_t)i;
+    HIPCHK(c, c->idx.ensure(m * 4));
+    HIPCHK(c, c->pk_all.ensure(m * blsk::G1_WORDS * 4));
+    HIPCHK(c, c->pk_all_inf.ensure(m));
+    HIPCHK(c, hipMemcpyAsync(c->idx.p, ident.data(), m * 4, hipMemcpyHostToDevice, c->stream));
+    blsk::launch_pubpoly_eval(c->commits.as<uint32_t>(), c->commit_inf.as<uint8_t>(), (uint32_t)t,
+                              c->idx.as<uint32_t>(), m, c->pk_all.as<uint32_t>(), c->pk_all_inf.as<uint8_t>(),
+                              c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // ident must outlive the copy
+    c->pk_all_n = m;
+  }
   c->t = t;
   c->n = n;
+  c->group_bytes.assign(commits48, commits48 + t * 48);
   c->has_group = true;
   return BLSV_OK;
 }
@@ -487,21 +513,29 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
   blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), k,
                              c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
   HIPCHK(c, c->idx.ensure(k * 4));
-  HIPCHK(c, c->pp_tab.ensure(k * blsk::G1_WORDS * 4));
-  HIPCHK(c, c->pp_inf.ensure(k));
-  HIPCHK(c, c->sel.ensure(k * 4));
   HIPCHK(c, hipMemcpyAsync(c->idx.p, index.data(), k * 4, hipMemcpyHostToDevice, c->stream));
-  std::vector<uint32_t> ident(k);
-  for (size_t i = 0; i < k; i++) ident[i] = (uint32_t)i;
-  HIPCHK(c, hipMemcpyAsync(c->sel.p, ident.data(), k * 4, hipMemcpyHostToDevice, c->stream));
-  blsk::launch_pubpoly_eval(c->commits.as<uint32_t>(), c->commit_inf.as<uint8_t>(), (uint32_t)c->t,
-                            c->idx.as<uint32_t>(), k, c->pp_tab.as<uint32_t>(), c->pp_inf.as<uint8_t>(), c->stream);
+  // PubPoly.Eval(index): the per-group table when every index is a member index (< n), else
+  // evaluated for this batch (an index >= n still has a well-defined Eval in kyber)
+  bool in_table = true;
+  for (size_t i = 0; i < k; i++) in_table = in_table && index[i] < c->pk_all_n;
+  std::vector<uint32_t> ident;
+  PkSel pk{c->pk_all.as<uint32_t>(), c->pk_all_inf.as<uint8_t>(), c->idx.as<uint32_t>()};
+  if (!in_table) {
+    HIPCHK(c, c->pp_tab.ensure(k * blsk::G1_WORDS * 4));
+    HIPCHK(c, c->pp_inf.ensure(k));
+    HIPCHK(c, c->sel.ensure(k * 4));
+    ident.resize(k);
+    for (size_t i = 0; i < k; i++) ident[i] = (uint32_t)i;
+    HIPCHK(c, hipMemcpyAsync(c->sel.p, ident.data(), k * 4, hipMemcpyHostToDevice, c->stream));
+    blsk::launch_pubpoly_eval(c->commits.as<uint32_t>(), c->commit_inf.as<uint8_t>(), (uint32_t)c->t,
+                              c->idx.as<uint32_t>(), k, c->pp_tab.as<uint32_t>(), c->pp_inf.as<uint8_t>(), c->stream);
+    pk = {c->pp_tab.as<uint32_t>(), c->pp_inf.as<uint8_t>(), c->sel.as<uint32_t>()};
+  }
   HIPCHK(c, c->in_sigs.ensure(k * partial_len + 96));
   HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, partials, k * partial_len, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, c->bitmap.ensure(((k + 63) / 64) * 8 + 8));
   HIPCHK(c, c->first_bad.ensure(8));
   HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
-  PkSel pk{c->pp_tab.as<uint32_t>(), c->pp_inf.as<uint8_t>(), c->sel.as<uint32_t>()};
   rc = run_tail(c, c->in_sigs.as<uint8_t>(), partial_len, 2, 0, k, pk, c->bitmap.as<uint64_t>(),
                 c->first_bad.as<unsigned long long>(), nullptr, c->stream);
   if (rc) return rc;
@@ -542,30 +576,36 @@ int blsv_verify_partials_multi(blsv_ctx* c, const uint8_t* msgs, const uint32_t*
   return BLSV_OK;
 }
 
-static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std::vector<uint32_t>& index, size_t k,
-                        size_t t, uint8_t* out_sig96);
+static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std::vector<uint32_t>& index, size_t lo,
+                        size_t hi, size_t t, size_t n, uint8_t* out_sig96);
 
 int blsv_recover(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
                  size_t k, size_t t, size_t n, uint8_t* out_sig96) {
   if (!c) return BLSV_EINVAL;
   if (!out_sig96 || t == 0 || (k && !partials)) return fail(c, BLSV_EINVAL, "recover: bad arguments");
-  (void)n;
   (void)hipSetDevice(c->device);
   std::vector<uint8_t> cls;
   std::vector<uint32_t> index;
   int rc = partials_stage(c, msg, msg_len, partials, partial_len, k, cls, index);
   if (rc) return rc;
-  return recover_from(c, cls, index, k, t, out_sig96);
+  return recover_from(c, cls, index, 0, k, t, n, out_sig96);
 }
 
-// Lagrange at 0 over the first t valid shares (input order; duplicate indices keep the first) of
-// the batch partials_stage just decompressed into c->S, then the G2 MSM and compression.
-static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std::vector<uint32_t>& index, size_t k,
-                        size_t t, uint8_t* out_sig96) {
+// kyber tbls.Recover + share.RecoverCommit ([ext] drand/kyber@d59c3367dcde sign/tbls/tbls.go,
+// share/poly.go, restated from the published source; parity unpinned by any reference test):
+// walk the shares of items [lo, hi) in input order, skip invalid ones, keep appending valid ones until
+// t are held -- a duplicate index counts toward t; then xyCommit keys them by index (duplicates
+// collapse) and drops indices >= n; fewer than t distinct -> "not enough good public shares".
+// Lagrange at 0 over those t shares (x = index + 1) of the batch partials_stage just decompressed
+// into c->S, then the G2 MSM and compression.
+static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std::vector<uint32_t>& index, size_t lo,
+                        size_t hi, size_t t, size_t n, uint8_t* out_sig96) {
   std::vector<uint32_t> sel, idx;
-  for (size_t i = 0; i < k && sel.size() < t; i++) {
+  size_t taken = 0;
+  for (size_t i = lo; i < hi && taken < t; i++) {
     if (cls[i] != BLSV_REJ_OK) continue;
-    if (std::find(idx.begin(), idx.end(), index[i]) != idx.end()) continue;
+    taken++;
+    if (index[i] >= n || std::find(idx.begin(), idx.end(), index[i]) != idx.end()) continue;
     sel.push_back((uint32_t)i);
     idx.push_back(index[i]);
   }
@@ -579,7 +619,7 @@ static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std:
   HIPCHK(c, hipMemcpyAsync(c->sel.p, sel.data(), t * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->idx.p, idx.data(), t * 4, hipMemcpyHostToDevice, c->stream));
   blsk::launch_lagrange(c->idx.as<uint32_t>(), (uint32_t)t, c->lambdas.as<uint32_t>(), c->stream);
-  blsk::launch_recover(c->S.as<uint32_t>(), k, c->s_inf.as<uint8_t>(), c->sel.as<uint32_t>(),
+  blsk::launch_recover(c->S.as<uint32_t>(), cls.size(), c->s_inf.as<uint8_t>(), c->sel.as<uint32_t>(),
                        c->lambdas.as<uint32_t>(), (uint32_t)t, c->scratch.as<uint32_t>(), c->out.as<uint8_t>(),
                        c->stream);
   HIPCHK(c, hipGetLastError());
@@ -594,7 +634,6 @@ int blsv_aggregate(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_
   if (!c) return BLSV_EINVAL;
   if (!out_sig96 || !ok || !group_ok || t == 0 || (k && !partials))
     return fail(c, BLSV_EINVAL, "aggregate: bad arguments");
-  (void)n;
   (void)hipSetDevice(c->device);
   std::vector<uint8_t> cls;
   std::vector<uint32_t> index;
@@ -605,7 +644,7 @@ int blsv_aggregate(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_
     if (reject_class) reject_class[i] = cls[i];
   }
   *group_ok = 0;
-  rc = recover_from(c, cls, index, k, t, out_sig96);
+  rc = recover_from(c, cls, index, 0, k, t, n, out_sig96);
   if (rc) return rc;
   // VerifyRecovered(group key, msg, sig) (chain/beacon/chain.go:141)
   const uint32_t len = (uint32_t)msg_len;
@@ -614,6 +653,74 @@ int blsv_aggregate(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_
   rc = blsv_verify_messages(c, nullptr, msg, &len, 1, out_sig96, &bm, &fb, &cls1);
   if (rc) return rc;
   *group_ok = bm & 1;
+  return BLSV_OK;
+}
+
+int blsv_aggregate_round(blsv_ctx* c, const uint8_t* msg1, size_t msg1_len, const uint8_t* partials1, size_t k1,
+                         const uint8_t* msg2, size_t msg2_len, const uint8_t* partials2, size_t k2,
+                         size_t partial_len, size_t t, size_t n, uint8_t* ok1, uint8_t* ok2, uint8_t* sig1_96,
+                         uint8_t* sig2_96, int32_t* status, uint8_t* v2_valid) {
+  if (!c) return BLSV_EINVAL;
+  if (!sig1_96 || !sig2_96 || !status || !v2_valid || t == 0 || (k1 && (!partials1 || !ok1)) ||
+      (k2 && (!partials2 || !ok2 || !msg2)) || (msg1_len && !msg1))
+    return fail(c, BLSV_EINVAL, "aggregate_round: bad arguments");
+  (void)hipSetDevice(c->device);
+  *status = BLSV_AGG_V1_RECOVER_FAIL;
+  *v2_valid = 0;
+  const size_t k = k1 + k2;
+  // pass 1: every V1 and V2 partial in ONE verification pass (per-item message)
+  std::vector<uint8_t> msgs, parts;
+  std::vector<uint32_t> lens(k);
+  msgs.reserve(k1 * msg1_len + k2 * msg2_len);
+  parts.reserve(k * partial_len);
+  for (size_t i = 0; i < k1; i++) {
+    msgs.insert(msgs.end(), msg1, msg1 + msg1_len);
+    lens[i] = (uint32_t)msg1_len;
+  }
+  for (size_t i = 0; i < k2; i++) {
+    msgs.insert(msgs.end(), msg2, msg2 + msg2_len);
+    lens[k1 + i] = (uint32_t)msg2_len;
+  }
+  if (k1) parts.insert(parts.end(), partials1, partials1 + k1 * partial_len);
+  if (k2) parts.insert(parts.end(), partials2, partials2 + k2 * partial_len);
+  std::vector<uint8_t> cls;
+  std::vector<uint32_t> index;
+  int rc = partials_stage(c, msgs.data(), 0, parts.data(), partial_len, k, cls, index, lens.data());
+  if (rc) return rc;
+  for (size_t i = 0; i < k1; i++) ok1[i] = cls[i] == BLSV_REJ_OK;
+  for (size_t i = 0; i < k2; i++) ok2[i] = cls[k1 + i] == BLSV_REJ_OK;
+  // Recover V1 (chain.go:136) and, with LenV2 >= thr, V2 (chain.go:153-155) from the staged shares
+  rc = recover_from(c, cls, index, 0, k1, t, n, sig1_96);
+  if (rc == BLSV_ENOTENOUGH) return BLSV_OK;  // "invalid_recovery": no beacon this time
+  if (rc) return rc;
+  const bool try_v2 = k2 >= t;
+  bool v2_recovered = false;
+  if (try_v2) {
+    rc = recover_from(c, cls, index, k1, k, t, n, sig2_96);
+    if (rc && rc != BLSV_ENOTENOUGH) return rc;
+    v2_recovered = rc == BLSV_OK;
+  }
+  // pass 2: VerifyRecovered(pub.Commit(), msg, sig) for both group signatures in one pass
+  const uint32_t vlens[2] = {(uint32_t)msg1_len, (uint32_t)msg2_len};
+  std::vector<uint8_t> vmsg(msg1, msg1 + msg1_len), vsig(sig1_96, sig1_96 + 96);
+  if (v2_recovered) {
+    vmsg.insert(vmsg.end(), msg2, msg2 + msg2_len);
+    vsig.insert(vsig.end(), sig2_96, sig2_96 + 96);
+  }
+  uint8_t bm = 0, vcls[2] = {0, 0};
+  uint64_t fb = 0;
+  rc = blsv_verify_messages(c, nullptr, vmsg.data(), vlens, v2_recovered ? 2 : 1, vsig.data(), &bm, &fb, vcls);
+  if (rc) return rc;
+  if (!(bm & 1)) {
+    *status = BLSV_AGG_V1_INVALID;  // chain.go:141-144 "invalid_sig": no beacon
+    return BLSV_OK;
+  }
+  if (try_v2 && !v2_recovered) {
+    *status = BLSV_AGG_V2_RECOVER_FAIL;  // chain.go:155-160: never accept a beacon with an invalid v2
+    return BLSV_OK;
+  }
+  *v2_valid = v2_recovered ? (uint8_t)((bm >> 1) & 1) : 0;  // chain.go:162-164: a failure only logs
+  *status = v2_recovered ? BLSV_AGG_OK_V2 : BLSV_AGG_OK;
   return BLSV_OK;
 }
 
@@ -644,20 +751,22 @@ int blsv_sign(blsv_ctx* c, const uint8_t* sk32, int32_t index, const uint8_t* ms
   return BLSV_OK;
 }
 
-int blsv_verify_chained_dev(blsv_ctx* c, uint64_t first_round, uint64_t seg_len, const uint8_t* d_seeds96,
-                            size_t seed0_len, const uint8_t* d_sigs96, size_t n, uint64_t* d_bitmap,
-                            uint64_t* d_first_bad, uint8_t* d_reject_class, void* stream) {
+int blsv_verify_chained_dev(blsv_ctx* c, uint64_t first_round, uint64_t seg_len, uint64_t seg_phase,
+                            const uint8_t* d_seeds96, size_t seed0_len, const uint8_t* d_sigs96, size_t n,
+                            uint64_t* d_bitmap, uint64_t* d_first_bad, uint8_t* d_reject_class, void* stream) {
   if (!c) return BLSV_EINVAL;
   if (!c->has_group) return fail(c, BLSV_ENOGROUP, "verify_chained_dev: no group key set");
   if (n && (!d_seeds96 || !d_sigs96 || !d_bitmap || !d_first_bad || (seed0_len != 32 && seed0_len != 96)))
     return fail(c, BLSV_EINVAL, "verify_chained_dev: bad arguments");
+  if (seg_phase && (!seg_len || seg_phase >= seg_len))
+    return fail(c, BLSV_EINVAL, "verify_chained_dev: seg_phase must be < seg_len");
   (void)hipSetDevice(c->device);
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   HIPCHK(c, hipMemsetAsync(d_first_bad, 0xff, 8, st));
   int rc = ensure_workspace(c, n);
   if (rc) return rc;
   blsk::ChainedSrc src{d_sigs96, d_seeds96, first_round, seg_len ? seg_len : std::max<uint64_t>(n, 1),
-                       (uint32_t)seed0_len};
+                       (uint32_t)seed0_len, seg_phase};
   for (size_t base = 0; base < n; base += c->cap) {
     const size_t cnt = std::min(c->cap, n - base);
     {

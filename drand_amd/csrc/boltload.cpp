@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <thread>
 #include <cstdio>
+#include <cctype>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -191,7 +192,9 @@ int parse_beacon(const uint8_t* p, size_t n, Fields& f, uint8_t* prev, uint8_t* 
         const uint8_t* ks = ++p;
         while (p < e && *p != '"') p++;
         if (p >= e) return -1;
+        // encoding/json (which hexjson forks) matches field names case-insensitively
         std::string key(reinterpret_cast<const char*>(ks), size_t(p - ks));
+        for (auto& ch : key) ch = char(std::tolower((unsigned char)ch));
         p = skip_ws(p + 1, e);
         if (p >= e || *p != ':') return -1;
         p = skip_ws(p + 1, e);
@@ -203,14 +206,18 @@ int parse_beacon(const uint8_t* p, size_t n, Fields& f, uint8_t* prev, uint8_t* 
             size_t vn = size_t(p - vs);
             p++;
             long len = 0;
-            if (key == "PreviousSig") len = f.prev_len = hexdecode(vs, vn, prev, 96);
-            else if (key == "Signature") len = f.sig_len = hexdecode(vs, vn, sig, 96);
-            else if (key == "SignatureV2") len = f.v2_len = hexdecode(vs, vn, v2, 96);
+            if (key == "previoussig") len = f.prev_len = hexdecode(vs, vn, prev, 96);
+            else if (key == "signature") len = f.sig_len = hexdecode(vs, vn, sig, 96);
+            else if (key == "signaturev2") len = f.v2_len = hexdecode(vs, vn, v2, 96);
             if (len < 0) return -1;
         } else if (*p >= '0' && *p <= '9') {
             uint64_t v = 0;
-            while (p < e && *p >= '0' && *p <= '9') v = v * 10 + uint64_t(*p++ - '0');
-            if (key == "Round") f.round = v;
+            while (p < e && *p >= '0' && *p <= '9') {
+                const uint64_t d = uint64_t(*p++ - '0');
+                if (v > (UINT64_MAX - d) / 10) return -1;  // json.Unmarshal: overflows uint64
+                v = v * 10 + d;
+            }
+            if (key == "round") f.round = v;
         } else if (e - p >= 4 && std::memcmp(p, "null", 4) == 0) {
             p += 4;
         } else {

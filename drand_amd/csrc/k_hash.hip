@@ -20,8 +20,8 @@ BLS_KERNEL(BLS_WPE_HASH) k_hash_chained(ChainedSrc src, size_t base, size_t cnt,
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt) return;
   const size_t g = base + i;
-  const size_t seg = g / src.seg_len;
-  const bool seg_start = (g - seg * src.seg_len) == 0;
+  const size_t seg = (g + src.seg_phase) / src.seg_len;
+  const bool seg_start = g == 0 || (g + src.seg_phase - seg * src.seg_len) == 0;
   const uint8_t* prev;
   int prev_len;
   if (seg_start) {

@@ -18,14 +18,18 @@ constexpr int F_WORDS = 144;  // Fp12
 constexpr int G1_WORDS = 24;  // affine G1 (x, y Montgomery), AoS entry in pk tables
 
 // Chained beacons (chain.VerifyBeacon with prev = the previous round's signature): item i has
-// round first_round + i; its prev is seeds[s] (s = i / seg_len, length seed0_len for s == 0 else
-// 96) when i % seg_len == 0, otherwise sigs[i-1]. seg_len = n gives one continuous chain.
+// round first_round + i; with s = (i + seg_phase) / seg_len its prev is seeds[s] (length seed0_len
+// for s == 0, else 96) when i == 0 or (i + seg_phase) % seg_len == 0, otherwise sigs[i-1].
+// seg_len = n gives one continuous chain. seg_phase (< seg_len) is the position of item 0 inside
+// its segment: a shard that starts mid-segment passes its halo (the true previous signature) as
+// seeds[0] and the following segment seeds as seeds[1..] (shard.py, bench.py --total-rounds).
 struct ChainedSrc {
   const uint8_t* sigs;   // n x 96 (global, whole batch)
   const uint8_t* seeds;  // n_seg x 96 slots
   uint64_t first_round;
   uint64_t seg_len;
   uint32_t seed0_len;  // 32 (genesis GroupHash) or 96
+  uint64_t seg_phase;  // 0 for the generator and every host-buffer entry point
 };
 
 void launch_hash_chained(const ChainedSrc& src, size_t base, size_t cnt, uint32_t* H, uint8_t* h_inf,

@@ -237,6 +237,29 @@ class Engine:
                                             out, gok))
         return [bool(x) for x in list(ok)[:k]], list(cls)[:k], bytes(out), bool(gok[0])
 
+    def aggregate_round(self, msg1, partials1, msg2, partials2, t, n):
+        """The aggregation step of one round cache, V1 + V2 (blsv_aggregate_round, chain.go:131-166):
+        returns (status AGG_*, ok1, ok2, sig1, sig2 or None, v2_valid)."""
+        k1, k2 = len(partials1), len(partials2)
+        plens = {len(p) for p in list(partials1) + list(partials2)} or {98}
+        if len(plens) != 1:
+            raise ValueError("partials of one call must share a length")
+        plen = plens.pop()
+        ok1, ok2 = _lib.out_buf(k1), _lib.out_buf(k2)
+        s1, s2 = _lib.out_buf(96), _lib.out_buf(96)
+        st = ctypes.c_int32()
+        v2 = _lib.out_buf(1)
+        self._check(self.lib.blsv_aggregate_round(
+            self._h, _lib.buf(msg1), len(msg1), _lib.buf(b"".join(bytes(p) for p in partials1)), k1,
+            _lib.buf(msg2), len(msg2), _lib.buf(b"".join(bytes(p) for p in partials2)), k2, plen, t, n, ok1, ok2,
+            s1, s2, ctypes.byref(st), v2))
+        status = st.value
+        sig1 = bytes(s1) if status in (_lib.AGG_OK, _lib.AGG_OK_V2, _lib.AGG_V1_INVALID,
+                                       _lib.AGG_V2_RECOVER_FAIL) else None
+        sig2 = bytes(s2) if status == _lib.AGG_OK_V2 else None
+        return (status, [bool(x) for x in list(ok1)[:k1]], [bool(x) for x in list(ok2)[:k2]], sig1, sig2,
+                bool(v2[0]))
+
     def sign(self, sk32, msgs, index=-1):
         n = len(msgs)
         lens = (ctypes.c_uint32 * max(n, 1))(*[len(m) for m in msgs])
@@ -249,9 +272,9 @@ class Engine:
 
     # ------------------------------------------------------------------ device-resident batches
     def verify_chained_dev(self, first_round, seg_len, d_seeds, seed0_len, d_sigs, n, d_bitmap, d_first_bad,
-                           d_cls=None, stream=None):
-        self._check(self.lib.blsv_verify_chained_dev(self._h, first_round, seg_len, d_seeds, seed0_len, d_sigs, n,
-                                                     d_bitmap, d_first_bad, d_cls, stream))
+                           d_cls=None, stream=None, seg_phase=0):
+        self._check(self.lib.blsv_verify_chained_dev(self._h, first_round, seg_len, seg_phase, d_seeds, seed0_len,
+                                                     d_sigs, n, d_bitmap, d_first_bad, d_cls, stream))
 
     def generate_chained_dev(self, sk32, first_round, seg_len, d_seeds, seed0_len, d_sigs, n, stream=None):
         self._check(self.lib.blsv_generate_chained_dev(self._h, _lib.buf(sk32), first_round, seg_len, d_seeds,

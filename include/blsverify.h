@@ -106,6 +106,30 @@ int blsv_aggregate(blsv_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint
                    size_t k, size_t t, size_t n, uint8_t* ok, uint8_t* reject_class, uint8_t* out_sig96,
                    uint8_t* group_ok);
 
+/* blsv_aggregate_round outcomes, in the order chain/beacon/chain.go:131-166 tests them */
+#define BLSV_AGG_OK 0              /* beacon made, V1 only (fewer than t V2 partials)                   */
+#define BLSV_AGG_OK_V2 1           /* beacon made with SignatureV2 (*v2_valid = VerifyRecovered V2)     */
+#define BLSV_AGG_V1_RECOVER_FAIL 2 /* Recover V1 failed (< t valid distinct shares): "invalid_recovery" */
+#define BLSV_AGG_V1_INVALID 3      /* VerifyRecovered V1 failed: "invalid_sig", no beacon                */
+#define BLSV_AGG_V2_RECOVER_FAIL 4 /* >= t V2 partials but Recover V2 failed: no beacon (chain.go:157)  */
+
+/*
+ * The whole aggregation step of chainStore.runAggregator (chain/beacon/chain.go:131-166) for one
+ * round cache, V1 and V2 together, in two verification passes: pass 1 checks the k1 V1 partials
+ * (roundCache.Partials(), msg1 = chain.Message(round, prev)) and the k2 V2 partials
+ * (roundCache.PartialsV2(), msg2 = chain.MessageV2(round)) in one batch (ok1/ok2); Recover V1 and,
+ * when k2 >= t, Recover V2 (kyber share selection, see blsv_recover) run on the staged shares; pass 2
+ * runs VerifyRecovered(pub.Commit(), ...) on both group signatures. *status = BLSV_AGG_*; sig1_96 /
+ * sig2_96 hold the group signatures when produced. A V2 VerifyRecovered failure does not block the
+ * beacon (*v2_valid = 0, chain.go:162-164); a V2 Recover failure does (chain.go:155-160). The
+ * threshold gate (roundCache.Len() >= thr) and the cache itself stay with the caller
+ * (drand_amd/callers.py Aggregator restates them).
+ */
+int blsv_aggregate_round(blsv_ctx* ctx, const uint8_t* msg1, size_t msg1_len, const uint8_t* partials1, size_t k1,
+                         const uint8_t* msg2, size_t msg2_len, const uint8_t* partials2, size_t k2,
+                         size_t partial_len, size_t t, size_t n, uint8_t* ok1, uint8_t* ok2, uint8_t* sig1_96,
+                         uint8_t* sig2_96, int32_t* status, uint8_t* v2_valid);
+
 /*
  * tbls.VerifyPartial (chain/beacon/node.go:112,125) over partials of MANY rounds in one pass:
  * partial i signs msgs[off_i .. off_i + msg_lens[i]) (messages packed back to back), e.g. a catch-up
@@ -142,9 +166,12 @@ int blsv_verify_partials(blsv_ctx* ctx, const uint8_t* msg, size_t msg_len, cons
 
 /*
  * key.Scheme.Recover(pubPoly, msg, sigs, t, n) (chain/beacon/chain.go:136,155): verifies the
- * partials, keeps the first t valid ones in input order (duplicate indices keep the first),
- * Lagrange-interpolates sum lambda_i sigma_i at 0 over x = index + 1 and writes the compressed
- * 96-byte group signature. Returns BLSV_ENOTENOUGH with fewer than t valid shares.
+ * partials and takes the first t VALID ones in input order, duplicates included (kyber tbls.Recover
+ * stops at len(pubShares) >= t); those are then keyed by index as share.RecoverCommit/xyCommit does
+ * (a duplicate collapses, an index >= n is dropped) and fewer than t distinct shares returns
+ * BLSV_ENOTENOUGH. Otherwise Lagrange-interpolates sum lambda_i sigma_i at 0 over x = index + 1 and
+ * writes the compressed 96-byte group signature. The skip-invalid / duplicate rules follow the
+ * published kyber source ([ext], unpinned by any reference test).
  */
 int blsv_recover(blsv_ctx* ctx, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
                  size_t k, size_t t, size_t n, uint8_t* out_sig96);
@@ -161,19 +188,25 @@ int blsv_sign(blsv_ctx* ctx, const uint8_t* sk32, int32_t index, const uint8_t* 
 
 /*
  * Chained verify over HBM-resident signatures, optionally split into independently seeded
- * segments of seg_len rounds (seg_len = 0 means one segment): beacon i (round first_round + i)
- * uses d_seeds96[s] as PreviousSig when i = s * seg_len (length seed0_len for s = 0, else 96),
- * else d_sigs96[i-1]. Outputs (device): d_bitmap (ceil(n/64) uint64 words, fully written),
- * d_first_bad (one uint64: the ROUND of the first reject or UINT64_MAX), d_reject_class (optional,
- * n bytes). Asynchronous on `stream` (a hipStream_t; NULL = the context stream).
+ * segments of seg_len rounds (seg_len = 0 means one segment): with s = (i + seg_phase) / seg_len,
+ * beacon i (round first_round + i) uses d_seeds96[s] as PreviousSig when i == 0 or
+ * (i + seg_phase) % seg_len == 0 (length seed0_len for s = 0, else 96), else d_sigs96[i-1].
+ * seg_phase (< seg_len; 0 when segments start at item 0) lets a shard that begins inside a
+ * segment pass its one-signature halo as d_seeds96[0] (multi-GPU range sharding).
+ * Outputs (device): d_bitmap (ceil(n/64) uint64 words, fully written), d_first_bad (one uint64:
+ * the ROUND of the first reject or UINT64_MAX), d_reject_class (optional, n bytes). Asynchronous
+ * on `stream` (a hipStream_t; NULL = the context stream). The context's staging buffers are shared
+ * by every call: successive *_dev calls on one context must be issued on ONE stream (or the caller
+ * orders them with events), never concurrently on two streams.
  */
-int blsv_verify_chained_dev(blsv_ctx* ctx, uint64_t first_round, uint64_t seg_len, const uint8_t* d_seeds96,
-                            size_t seed0_len, const uint8_t* d_sigs96, size_t n, uint64_t* d_bitmap,
-                            uint64_t* d_first_bad, uint8_t* d_reject_class, void* stream);
+int blsv_verify_chained_dev(blsv_ctx* ctx, uint64_t first_round, uint64_t seg_len, uint64_t seg_phase,
+                            const uint8_t* d_seeds96, size_t seed0_len, const uint8_t* d_sigs96, size_t n,
+                            uint64_t* d_bitmap, uint64_t* d_first_bad, uint8_t* d_reject_class, void* stream);
 
 /*
  * Synthetic chained history (client/test/result/mock/result.go:98-132, per segment, on device):
- * d_sigs96[i] = compress(sk * H(Message(first_round + i, prev))) with the seed rule above.
+ * d_sigs96[i] = compress(sk * H(Message(first_round + i, prev))) with the seed rule above
+ * (seg_phase = 0). Same single-stream rule as blsv_verify_chained_dev.
  */
 int blsv_generate_chained_dev(blsv_ctx* ctx, const uint8_t* sk32, uint64_t first_round, uint64_t seg_len,
                               const uint8_t* d_seeds96, size_t seed0_len, uint8_t* d_sigs96, size_t n, void* stream);

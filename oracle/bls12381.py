@@ -747,20 +747,25 @@ def tbls_verify_partial(commits, msg, partial):
 
 
 def tbls_recover(commits, msg, partials, t, n):
-    """tbls.Recover -> share.RecoverCommit: keep the first t *valid* shares in input order
-    (duplicate indices keep the first), Lagrange-interpolate at 0 over x = i+1, compress."""
-    shares = {}
+    """tbls.Recover -> share.RecoverCommit ([ext] drand/kyber@d59c3367dcde, restated from the
+    published source; parity unpinned by any reference test): walk the shares in input order, skip
+    invalid ones, append valid ones until t are held (a duplicate index COUNTS toward t); xyCommit
+    then keys them by index (duplicates collapse) and drops indices >= n; fewer than t distinct ->
+    "not enough good public shares". Lagrange-interpolate at 0 over x = i+1, compress."""
+    taken = []
     for ps in partials:
-        if len(shares) >= t:
+        if len(taken) >= t:
             break
         try:
             i = tbls_index_of(ps)
-            if i in shares:
-                continue
             tbls_verify_partial(commits, msg, ps)
-            shares[i] = g2_decompress(bytes(ps[2:]))
+            taken.append((i, g2_decompress(bytes(ps[2:]))))
         except VerifyError:
             continue
+    shares = {}
+    for i, pt in taken:
+        if 0 <= i < n:
+            shares[i] = pt
     if len(shares) < t:
         raise VerifyError("share: not enough good public shares to reconstruct secret commitment")
     xs = {i: (i + 1) % R for i in shares}

@@ -142,9 +142,16 @@ def threshold(label, n, t, rng):
     assert rec == group_sig, "recover != a0*H(m)"
     # a corrupted partial (valid point, wrong share) for the negative path
     bad = O.tbls_sign(3, (O.pripoly_eval(coeffs, 3) + 1) % O.R, msg)
+    # the same round's V2 partials (node.go:298-299: SignPartial over MessageV2(round)); no rng draws
+    msg2 = O.message_v2(rnd)
+    partials_v2 = [O.tbls_sign(i, O.pripoly_eval(coeffs, i), msg2) for i in range(n)]
+    group_sig_v2 = O.sign(coeffs[0], msg2)
+    bad_v2 = O.tbls_sign(5, (O.pripoly_eval(coeffs, 5) + 1) % O.R, msg2)
     return {"label": label, "n": n, "t": t, "round": rnd, "prev": hx(prev), "msg": hx(msg),
             "commits": [hx(O.g1_compress(c)) for c in commits], "partials": [hx(p) for p in partials],
-            "recover_subset": [hx(p) for p in shuffled], "group_sig": hx(group_sig), "bad_partial": hx(bad)}
+            "recover_subset": [hx(p) for p in shuffled], "group_sig": hx(group_sig), "bad_partial": hx(bad),
+            "msg_v2": hx(msg2), "partials_v2": [hx(p) for p in partials_v2], "group_sig_v2": hx(group_sig_v2),
+            "bad_partial_v2": hx(bad_v2)}
 
 
 def main():

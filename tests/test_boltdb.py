@@ -70,6 +70,16 @@ def test_meta_selection_and_errors(tmp_path, chain):
     write_db(p, [(struct.pack(">Q", 1), b'{"Round":1,"Signature":"zz"}')])
     with pytest.raises(boltdb.StoreError, match="malformed"):
         boltdb.load_store(p)
+    # a Round that overflows uint64 is a json.Unmarshal error, not a silent wrap
+    write_db(p, [(struct.pack(">Q", 1), b'{"Round":18446744073709551617,"Signature":"00"}')])
+    with pytest.raises(boltdb.StoreError, match="malformed"):
+        boltdb.load_store(p)
+    # field names match case-insensitively, as encoding/json (hexjson) does
+    b0 = bs[0]
+    write_db(p, [(struct.pack(">Q", 1), b'{"previoussig":"%s","ROUND":1,"signature":"%s"}'
+                  % (b0.previous_sig.hex().encode(), b0.signature.hex().encode()))])
+    sb = boltdb.load_store(p)
+    assert sb.rounds.tolist() == [1] and sb.sigs[0].tobytes() == b0.signature and sb.prev_len[0] == 32
     # not a bbolt file
     p.write_bytes(b"\0" * 8192)
     with pytest.raises(boltdb.StoreError, match="meta"):
@@ -119,6 +129,34 @@ def test_verify_store_cpu(tmp_path, chain):
 @pytest.mark.gpu
 def test_verify_store_gpu(tmp_path, chain, engine):
     _check_verdicts(engine, tmp_path, chain)
+
+
+def _genesis_item(group_hash):
+    # chain.GenesisBeacon (chain/store.go:234-238) as Put at node start (chain/beacon/node.go:69):
+    # Round 0, nil PreviousSig (hexjson null), Signature = GroupHash (32 bytes)
+    return (struct.pack(">Q", 0), b'{"PreviousSig":null,"Round":0,"Signature":"%s"}' % group_hash.hex().encode())
+
+
+@pytest.mark.parametrize("tamper", [False, True])
+def test_genesis_row_is_trusted_root(tmp_path, chain, tamper):
+    """every real drand.db starts with the round-0 genesis beacon; it is never verified
+    (sync starts at last+1, the client walk at round 1), so it must not become first_bad."""
+    pk, seed, bs = chain
+    bs = _tampered(bs) if tamper else bs
+    p = tmp_path / "g.db"
+    write_db(p, [_genesis_item(seed)] + _items(bs), per_leaf=3)
+    sb = boltdb.load_store(p)
+    assert sb.rounds[0] == 0 and sb.prev_len[0] == 0 and sb.sig_len[0] == 32
+    eng = OracleEngine()
+    v = boltdb.verify_store(eng, pk, sb, group_hash=seed)
+    assert v.ok[0]
+    assert all(c[1] != 0 for c in eng.calls)  # round 0 never reaches the engine
+    assert v.first_bad == (10 if tamper else None)
+    assert sorted(sb.rounds[~v.ok].tolist()) == ([10, 16] if tamper else [])
+    v = boltdb.verify_store(eng, pk, sb)  # no GroupHash given: trusted as is
+    assert v.ok[0] and v.first_bad == (10 if tamper else None)
+    v = boltdb.verify_store(eng, pk, sb, group_hash=bytes(32))  # wrong GroupHash: flagged, not first_bad
+    assert not v.ok[0] and v.first_bad == (10 if tamper else None)
 
 
 def test_parallel_decode_reports_lowest_bad_entry(tmp_path, chain, monkeypatch):

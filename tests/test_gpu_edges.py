@@ -80,13 +80,37 @@ def test_recover_selection_rules(engine, golden):
         assert engine.recover(msg, sub, t, th["n"]).hex() == th["group_sig"]
     bad = bytes.fromhex(th["bad_partial"])
     dup = partials[0]
-    # invalid shares and duplicate indices are skipped, the next valid ones complete the set
-    sub = [bad, dup, dup] + partials[1:t]
+    # invalid shares are skipped, the next valid ones complete the set
+    sub = [bad, dup] + partials[1:t]
     assert engine.recover(msg, sub, t, th["n"]).hex() == th["group_sig"]
     # fewer than t valid shares -> BLSV_ENOTENOUGH
     with pytest.raises(EngineError) as e:
         engine.recover(msg, [bad] + partials[: t - 1], t, th["n"])
     assert e.value.code == _lib.BLSV_ENOTENOUGH
+    # PARITY UNPINNED ([ext] kyber tbls.Recover / share.xyCommit, restated from the published
+    # source): a duplicate index among the first t valid shares counts toward t and then
+    # collapses -> not enough distinct shares, even though a later share would have completed the set
+    with pytest.raises(EngineError) as e:
+        engine.recover(msg, [bad, dup, dup] + partials[1:t], t, th["n"])
+    assert e.value.code == _lib.BLSV_ENOTENOUGH
+
+
+def test_recover_index_beyond_n_parity_unpinned(engine, golden):
+    """PARITY UNPINNED (xyCommit drops s.I >= n): a single-key group (t = 1, Eval(i) = C0 for every
+    i) accepts a share at index 5 as VALID, but Recover with n = 1 drops it -> ENOTENOUGH; index 0
+    recovers the signature itself (lambda = 1)."""
+    import hashlib
+    ch = golden["chained"]
+    b = ch["beacons"][0]
+    msg = hashlib.sha256(bytes.fromhex(b["prev"]) + b["round"].to_bytes(8, "big")).digest()
+    sig = bytes.fromhex(b["sig"])
+    engine.set_group([bytes.fromhex(ch["pk"])], 1)
+    assert engine.verify_partials(msg, [b"\0\5" + sig])[0] == [True]
+    with pytest.raises(EngineError) as e:
+        engine.recover(msg, [b"\0\5" + sig], 1, 1)
+    assert e.value.code == _lib.BLSV_ENOTENOUGH
+    assert engine.recover(msg, [b"\0\0" + sig], 1, 1) == sig
+    assert engine.recover(msg, [b"\0\5" + sig], 1, 6) == sig
 
 
 @pytest.mark.gpu

@@ -119,3 +119,44 @@ def test_unchained_batch_signed_on_device(engine, golden):
     assert all(res.ok) and res.first_bad is None
     res = engine.verify_unchained(sigs, first_round=first + 1)
     assert not any(res.ok) and res.first_bad == first + 1
+
+
+def test_sharded_slices_with_phase_match_whole(engine, golden):
+    """configs[3] path on one GPU: one segmented history verified whole, then as 3 and 5 contiguous
+    shards that start mid-segment (seg_phase, halo = the true previous signature as seeds[0], exactly
+    what bench.py --total-rounds does per rank); the re-assembled verdicts equal the whole-history
+    verdicts, including a corrupted signature just before a shard boundary (its successor, the next
+    shard's first round, must reject through the halo)."""
+    import torch
+
+    from drand_amd import shard
+
+    n, seg = 9001, 64
+    seeds, sigs, s0 = _history(engine, golden, n, seg, seed=21)
+    S = sigs.view(n, 96)
+    Q = seeds.view(-1, 96)
+    for world in (3, 5):
+        cut = shard.shard_range(n, world, 1).start - 1  # last round of shard 0
+        host = sigs.cpu()
+        host[cut * 96 + 50] ^= 1
+        bad_sigs = host.to("cuda:0")
+        ok_whole, fb_whole, _ = _verify(engine, 1, seg, seeds, s0, bad_sigs, n)
+        assert fb_whole == cut + 1
+        S = bad_sigs.view(n, 96)
+        got = []
+        for r in range(world):
+            sl = shard.segmented_slice(n, world, r, seg)
+            gen_sigs = S[sl.gen_start:sl.gen_start + sl.gen_count]
+            loc = shard.local_seeds(sl, Q[sl.seg_first:sl.seg_first + sl.n_seg], gen_sigs)
+            mine = S[sl.shard.start:sl.shard.start + sl.shard.count].contiguous()
+            c = sl.shard.count
+            bitmap = torch.zeros((c + 63) // 64, dtype=torch.int64, device="cuda:0")
+            fb = torch.empty(1, dtype=torch.int64, device="cuda:0")
+            engine.verify_chained_dev(sl.shard.first_round, seg, loc.data_ptr(), 32 if sl.shard.start == 0 else 96,
+                                      mine.data_ptr(), c, bitmap.data_ptr(), fb.data_ptr(), None, None,
+                                      seg_phase=sl.phase)
+            torch.cuda.synchronize()
+            bm = [w & NONE for w in bitmap.cpu().tolist()]
+            got += [(bm[i // 64] >> (i % 64)) & 1 == 1 for i in range(c)]
+        assert got == ok_whole
+        assert not got[cut] and (not got[cut + 1] or (cut + 1) % seg == 0)
