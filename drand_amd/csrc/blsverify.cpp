@@ -863,6 +863,33 @@ int blsv_test_pairing(blsv_ctx* c, const uint32_t* p, const uint32_t* q, size_t 
   return BLSV_OK;
 }
 
+int blsv_test_final_exp(blsv_ctx* c, const uint32_t* f, size_t n, uint32_t* out_pipeline, uint32_t* out_ref) {
+  if (!c || (n && (!f || !out_pipeline || !out_ref))) return BLSV_EINVAL;
+  if (n > kMaxChunk) return BLSV_EINVAL;
+  (void)hipSetDevice(c->device);
+  int rc = ensure_workspace(c, n);
+  if (rc) return rc;
+  if (!n) return BLSV_OK;
+  DBuf din, dout, dref;
+  HIPCHK(c, din.ensure(n * 576));
+  HIPCHK(c, dout.ensure(n * 576));
+  HIPCHK(c, dref.ensure(n * 576));
+  HIPCHK(c, hipMemcpyAsync(din.p, f, n * 576, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->cls.p, 0, n, c->stream));
+  blsk::launch_test_pack_fp12(din.as<uint32_t>(), n, c->F.as<uint32_t>(), c->stream);
+  blsk::launch_test_final_exp_ref(c->F.as<uint32_t>(), n, dref.as<uint32_t>(), c->stream);
+  // the production stage (clobbers F), its final value captured into dout
+  blsk::launch_final_exp(c->F.as<uint32_t>(), c->FW.as<uint32_t>(), n, c->cls.as<uint8_t>(), c->stream,
+                         dout.as<uint32_t>());
+  blsk::launch_test_unpack_fp12(dout.as<uint32_t>(), n, din.as<uint32_t>(), c->stream);
+  HIPCHK(c, hipMemcpyAsync(out_pipeline, din.p, n * 576, hipMemcpyDeviceToHost, c->stream));
+  blsk::launch_test_unpack_fp12(dref.as<uint32_t>(), n, dout.as<uint32_t>(), c->stream);
+  HIPCHK(c, hipMemcpyAsync(out_ref, dout.p, n * 576, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
 int blsv_test_hash_to_g2(blsv_ctx* c, const uint8_t* msgs, const uint32_t* msg_lens, size_t n, uint32_t* out,
                          uint8_t* inf) {
   if (!c || (n && (!msg_lens || !out || !inf))) return BLSV_EINVAL;

@@ -353,20 +353,10 @@ DI void fp2_arg_store(const u24& b) {
   for (int i = 0; i < 24; i++) g_fp2_arg[i * BLS_LANES + l] = b[i];
 }
 
-// Fp2 product (a0 + a1 i)(b0 + b1 i), b from fp2_arg_store, in one call:
+// Fp2 product (a0 + a1 i)(b0 + b1 i) in one body:
 //   c0 = a0 b0 + a1 (4p - b1), c1 = a0 b1 + a1 b0
 // i.e. two reductions instead of three multiplications' worth (counted as the 3 of Karatsuba).
-NOINL u24 fp2_mul_u24(u24 a) {
-  BLS_COUNT_MUL();
-  BLS_COUNT_MUL();
-  BLS_COUNT_MUL();
-  const unsigned l = bls_lane();
-  u12 b0, b1;
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    b0[i] = g_fp2_arg[i * BLS_LANES + l];
-    b1[i] = g_fp2_arg[(12 + i) * BLS_LANES + l];
-  }
+DI u24 fp2_mul_body(const u24& a, const u12& b0, const u12& b1) {
   uint32_t x0[14], x1[14], y0[14], y1[14];
   fp_split28(u24_lo(a), x0);
   fp_split28(u24_hi(a), x1);
@@ -380,9 +370,7 @@ NOINL u24 fp2_mul_u24(u24 a) {
 }
 
 // Fp2 square: c0 = (a0 + a1)(a0 + 4p - a1), c1 = (2 a0) a1
-NOINL u24 fp2_sqr_u24(u24 a) {
-  BLS_COUNT_MUL();
-  BLS_COUNT_MUL();
+DI u24 fp2_sqr_body(const u24& a) {
   const u12 a0 = u24_lo(a), a1 = u24_hi(a);
   uint32_t x[14], y[14];
   fp_split28(fp_add_raw_u12(a0, a1), x);
@@ -393,6 +381,29 @@ NOINL u24 fp2_sqr_u24(u24 a) {
   fp_split28(a1, y);
   const u12 c1 = fp_mont_dot<false>(x, y, x, y);
   return u24_of(c0, c1);
+}
+
+// The called forms: b of fp2_mul_u24 comes from fp2_arg_store (LDS), one copy of each body per
+// code object. The _inl forms (tower.h fp2_mul_inl / fp2_sqr_inl) expand the bodies in place for
+// call-free hot loops (the 3-lane final exponentiation, tri.h).
+NOINL u24 fp2_mul_u24(u24 a) {
+  BLS_COUNT_MUL();
+  BLS_COUNT_MUL();
+  BLS_COUNT_MUL();
+  const unsigned l = bls_lane();
+  u12 b0, b1;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    b0[i] = g_fp2_arg[i * BLS_LANES + l];
+    b1[i] = g_fp2_arg[(12 + i) * BLS_LANES + l];
+  }
+  return fp2_mul_body(a, b0, b1);
+}
+
+NOINL u24 fp2_sqr_u24(u24 a) {
+  BLS_COUNT_MUL();
+  BLS_COUNT_MUL();
+  return fp2_sqr_body(a);
 }
 
 DI u12 fp_to_u12(const fp& a) {

@@ -32,21 +32,85 @@ BLS_KERNEL(BLS_WPE_FEXP) k_fexp_step(const uint32_t* X, const uint32_t* C, const
   }
 }
 
+// ------------------------------------------------------------------ 3-lane hard part (tri.h)
+// Same fexp_step<MODE> sequence, each Fp12 spread over 3 lanes (Fp4 thirds): the 63 cyclotomic
+// squares per exponentiation are call-free (3 in-place Fp2 squares per lane), the 5 multiplications
+// use the called Fp2 product. 21 beacons per wave.
+#ifndef BLS_WPE_FEXP_TRI
+#define BLS_WPE_FEXP_TRI 2
+#endif
+
+template <typename LoadX>
+DI fp4 tri_pow_x_abs(const tri_lane& t, LoadX lx) {
+  constexpr uint64_t NSQ = 1ull | (2ull << 6) | (3ull << 12) | (9ull << 18) | (32ull << 24) | (16ull << 30);
+  fp4 r = lx();
+#pragma unroll 1
+  for (int s = 0; s < 6; s++) {
+    const int n = (int)((NSQ >> (6 * s)) & 63u);
+#pragma unroll 1
+    for (int k = 0; k < n; k++) r = tri_cyclotomic_sqr(t, r);
+    if (s < 5) r = tri_mul(t, r, lx());
+  }
+  return r;
+}
+
+template <int MODE>
+BLS_KERNEL(BLS_WPE_FEXP_TRI) k_fexp_tri(const uint32_t* X, const uint32_t* C, const uint32_t* G, size_t cnt,
+                                        uint8_t* cls, uint32_t* OUT) {
+  const tri_lane t = tri_lane_id();
+  const size_t ir = (size_t)blockIdx.x * TRI_GROUPS + t.group;
+  const bool in_range = t.group < TRI_GROUPS && ir < cnt;
+  const size_t i0 = in_range ? ir : cnt - 1;  // dummy lanes compute on a real row, never store
+  const bool live = in_range && cls[i0] == REJ_OK;
+  // every lane stays active to the end (ds_bpermute reads its partners' registers)
+  auto at = [&](const uint32_t* B) {
+    size_t j = i0;
+    asm volatile("" : "+v"(j));  // re-read at each use, never hoisted (as in k_fexp_step)
+    return tri_load(B, cnt, j, t.role);
+  };
+  fp4 r = tri_conj(t, tri_pow_x_abs(t, [&]() { return at(X); }));
+  if (MODE == 0 || MODE == 1) r = tri_mul(t, r, tri_conj(t, at(X)));
+  if (MODE == 2) r = tri_mul(t, r, tri_frob(t, at(X)));
+  if (MODE == 4) {
+    r = tri_mul(t, r, tri_frob2(t, at(C)));
+    r = tri_mul(t, r, tri_conj(t, at(C)));
+    r = tri_mul(t, r, tri_cyclotomic_sqr(t, at(G)));
+    r = tri_mul(t, r, at(G));
+  }
+  if (MODE < 4 || OUT) {  // MODE 4 with OUT: the final value too (blsv_test_final_exp)
+    if (live) tri_store(OUT, cnt, i0, t.role, r);
+  }
+  if (MODE == 4) {
+    const bool one = tri_is_one(t, r);
+    if (live && t.role == 0 && !one) cls[i0] = REJ_PAIRING;
+  }
+}
+
 // ------------------------------------------------------------------ launchers
 // F (Miller output) is consumed by the easy part and then reused as scratch; W holds 3 more Fp12
 // staging slots of cnt entries each (G, B, C).
-void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st) {
+void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st, uint32_t* out) {
   if (!cnt) return;
   uint32_t* G = W;
   uint32_t* B = W + cnt * F_WORDS;
   uint32_t* C = W + 2 * cnt * F_WORDS;
   const dim3 grid(grid_for(cnt)), blk(TPB);
   hipLaunchKernelGGL(k_fexp_easy, grid, blk, 0, st, F, cnt, cls, G);
+#ifdef BLS_FEXP_SINGLE_LANE
   hipLaunchKernelGGL(k_fexp_step<0>, grid, blk, 0, st, G, nullptr, nullptr, cnt, cls, F);  // a -> F
   hipLaunchKernelGGL(k_fexp_step<1>, grid, blk, 0, st, F, nullptr, nullptr, cnt, cls, B);  // b -> B
   hipLaunchKernelGGL(k_fexp_step<2>, grid, blk, 0, st, B, nullptr, nullptr, cnt, cls, C);  // c -> C
   hipLaunchKernelGGL(k_fexp_step<3>, grid, blk, 0, st, C, nullptr, nullptr, cnt, cls, F);  // t -> F
   hipLaunchKernelGGL(k_fexp_step<4>, grid, blk, 0, st, F, C, G, cnt, cls, nullptr);
+  (void)out;
+#else
+  const dim3 tgrid((unsigned)((cnt + TRI_GROUPS - 1) / TRI_GROUPS));
+  hipLaunchKernelGGL(k_fexp_tri<0>, tgrid, blk, 0, st, G, nullptr, nullptr, cnt, cls, F);  // a -> F
+  hipLaunchKernelGGL(k_fexp_tri<1>, tgrid, blk, 0, st, F, nullptr, nullptr, cnt, cls, B);  // b -> B
+  hipLaunchKernelGGL(k_fexp_tri<2>, tgrid, blk, 0, st, B, nullptr, nullptr, cnt, cls, C);  // c -> C
+  hipLaunchKernelGGL(k_fexp_tri<3>, tgrid, blk, 0, st, C, nullptr, nullptr, cnt, cls, F);  // t -> F
+  hipLaunchKernelGGL(k_fexp_tri<4>, tgrid, blk, 0, st, F, C, G, cnt, cls, out);
+#endif
 }
 
 }  // namespace blsk

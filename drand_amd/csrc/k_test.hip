@@ -61,7 +61,51 @@ __global__ void k_test_unpack_g2(const uint32_t* H, size_t cnt, uint32_t* out) {
   }
 }
 
+// raw AoS Fp12 (144 words, tower order) <-> Montgomery SoA staging (soa.h slot order is the same)
+__global__ void k_test_pack_fp12(const uint32_t* f, size_t cnt, uint32_t* F) {
+  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= cnt) return;
+  for (int s = 0; s < 12; s++) {
+    fp v;
+#pragma unroll
+    for (int w = 0; w < 12; w++) v.l[w] = f[i * 144 + s * 12 + w];
+    st_fp(F, cnt, i, s, fp_to_mont(v));
+  }
+}
+
+__global__ void k_test_unpack_fp12(const uint32_t* F, size_t cnt, uint32_t* out) {
+  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= cnt) return;
+  for (int s = 0; s < 12; s++) {
+    fp v = fp_from_mont(ld_fp(F, cnt, i, s));
+#pragma unroll
+    for (int w = 0; w < 12; w++) out[i * 144 + s * 12 + w] = v.l[w];
+  }
+}
+
+// one-lane register final exponentiation (pairing.h final_exponentiation) on SoA staging
+__global__ void __launch_bounds__(TPB) k_test_final_exp_ref(const uint32_t* F, size_t cnt, uint32_t* out) {
+  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= cnt) return;
+  st_fp12(out, cnt, i, final_exponentiation(ld_fp12(F, cnt, i)));
+}
+
 // ------------------------------------------------------------------ launchers
+void launch_test_pack_fp12(const uint32_t* f, size_t cnt, uint32_t* F, hipStream_t st) {
+  if (!cnt) return;
+  hipLaunchKernelGGL(k_test_pack_fp12, dim3(grid_for(cnt)), dim3(TPB), 0, st, f, cnt, F);
+}
+
+void launch_test_unpack_fp12(const uint32_t* F, size_t cnt, uint32_t* out, hipStream_t st) {
+  if (!cnt) return;
+  hipLaunchKernelGGL(k_test_unpack_fp12, dim3(grid_for(cnt)), dim3(TPB), 0, st, F, cnt, out);
+}
+
+void launch_test_final_exp_ref(const uint32_t* F, size_t cnt, uint32_t* out, hipStream_t st) {
+  if (!cnt) return;
+  hipLaunchKernelGGL(k_test_final_exp_ref, dim3(grid_for(cnt)), dim3(TPB), 0, st, F, cnt, out);
+}
+
 void launch_test_fp_mul(const uint32_t* a, const uint32_t* b, size_t cnt, uint32_t* out, hipStream_t st) {
   if (!cnt) return;
   hipLaunchKernelGGL(k_test_fp_mul, dim3(grid_for(cnt)), dim3(TPB), 0, st, a, b, cnt, out);

@@ -4,6 +4,7 @@
 #include "hash.h"
 #include "pairing.h"
 #include "soa.h"
+#include "tri.h"
 
 namespace blsk {
 using namespace bls;

@@ -49,8 +49,9 @@ constexpr int MILLER_LINE_WORDS = 68 * 2 * 6 * 12;
 void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
                    const uint8_t* h_inf, const uint32_t* S, const uint8_t* s_inf, const uint8_t* cls, size_t cnt,
                    uint32_t* F, uint32_t* LN, size_t sub, hipStream_t st);
-// F is clobbered; W = 3 * cnt * F_WORDS words of staging
-void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st);
+// F is clobbered; W = 3 * cnt * F_WORDS words of staging; out (optional, test hook): the
+// exponentiated values (SoA, cnt * F_WORDS words)
+void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st, uint32_t* out = nullptr);
 // bitmap bit (base+i) = (cls[i] == 0); bitmap must cover whole 64-bit words;
 // first_bad = label0 + min rejected index (label0 = first_round -> ROUND numbers)
 void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap, unsigned long long* first_bad,
@@ -79,5 +80,10 @@ void launch_gen_chained(const uint32_t* sk_words, const ChainedSrc& src, size_t 
 void launch_test_fp_mul(const uint32_t* a, const uint32_t* b, size_t cnt, uint32_t* out, hipStream_t st);
 void launch_test_pairing(const uint32_t* p_tab, const uint32_t* q_aff, size_t cnt, uint32_t* out_f, hipStream_t st);
 void launch_test_unpack_g2(const uint32_t* H, size_t cnt, uint32_t* out, hipStream_t st);
+// raw AoS Fp12 (144 words each, tower order) <-> Montgomery SoA staging
+void launch_test_pack_fp12(const uint32_t* f, size_t cnt, uint32_t* F, hipStream_t st);
+void launch_test_unpack_fp12(const uint32_t* F, size_t cnt, uint32_t* out, hipStream_t st);
+// SoA F -> final_exponentiation(F) with the one-lane register form (pairing.h), SoA out
+void launch_test_final_exp_ref(const uint32_t* F, size_t cnt, uint32_t* out, hipStream_t st);
 
 }  // namespace blsk

@@ -43,6 +43,18 @@ DI fp2 fp2_mul(const fp2& a, const fp2& b) {
   return fp2_from_u24(fp2_mul_u24(fp2_to_u24(a)));
 }
 DI fp2 fp2_sqr(const fp2& a) { return fp2_from_u24(fp2_sqr_u24(fp2_to_u24(a))); }
+// in-place expansions (no call): for call-free kernels whose register budget must stay small
+DI fp2 fp2_mul_inl(const fp2& a, const fp2& b) {
+  BLS_COUNT_MUL();
+  BLS_COUNT_MUL();
+  BLS_COUNT_MUL();
+  return fp2_from_u24(fp2_mul_body(fp2_to_u24(a), fp_to_u12(b.c0), fp_to_u12(b.c1)));
+}
+DI fp2 fp2_sqr_inl(const fp2& a) {
+  BLS_COUNT_MUL();
+  BLS_COUNT_MUL();
+  return fp2_from_u24(fp2_sqr_body(fp2_to_u24(a)));
+}
 
 DI fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
 DI fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1)}; }

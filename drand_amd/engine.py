@@ -314,6 +314,15 @@ class Engine:
         self._check(self.lib.blsv_test_pairing(self._h, Pp, Q, n, O))
         return list(O)[:n * 144]
 
+    def test_final_exp(self, f_words):
+        """(production stage, one-lane reference) final exponentiations of n Fp12 (144 raw words each)."""
+        n = len(f_words) // 144
+        Fw = (ctypes.c_uint32 * max(len(f_words), 1))(*f_words)
+        A = (ctypes.c_uint32 * max(n * 144, 1))()
+        B = (ctypes.c_uint32 * max(n * 144, 1))()
+        self._check(self.lib.blsv_test_final_exp(self._h, Fw, n, A, B))
+        return list(A)[:n * 144], list(B)[:n * 144]
+
     def test_hash_to_g2(self, msgs):
         n = len(msgs)
         lens = (ctypes.c_uint32 * max(n, 1))(*[len(m) for m in msgs])

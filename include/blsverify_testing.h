@@ -22,6 +22,13 @@ int blsv_test_fp_mul(blsv_ctx* ctx, const uint32_t* a, const uint32_t* b, size_t
  */
 int blsv_test_pairing(blsv_ctx* ctx, const uint32_t* p, const uint32_t* q, size_t n, uint32_t* out_f);
 
+/*
+ * The production final-exponentiation stage (drand_amd/csrc/k_fexp.hip: the 3-lane hard part) and
+ * the one-lane register form (pairing.h final_exponentiation) on the same n inputs f[i] (144 raw
+ * words each, tower order as in blsv_test_pairing): out_pipeline[i] and out_ref[i] must agree.
+ */
+int blsv_test_final_exp(blsv_ctx* ctx, const uint32_t* f, size_t n, uint32_t* out_pipeline, uint32_t* out_ref);
+
 /* out[i] = H(msg_i) as affine raw words (x.c0, x.c1, y.c0, y.c1; 48 words) + inf flag. */
 int blsv_test_hash_to_g2(blsv_ctx* ctx, const uint8_t* msgs, const uint32_t* msg_lens, size_t n, uint32_t* out,
                          uint8_t* inf);

@@ -131,3 +131,24 @@ def test_threshold_partials_and_recover(engine, golden):
     # the group signature verifies under commits[0] (VerifyRecovered, chain/beacon/chain.go:141)
     res = engine.verify_messages([msg], [sig])
     assert res.ok == [True]
+
+
+def test_final_exp_tri_matches_one_lane(engine):
+    """The production final exponentiation (3 lanes per Fp12, k_fexp_tri) equals the one-lane
+    register form (pairing.h final_exponentiation, itself pinned by the pairing goldens) on random
+    Fp12 values, including batches that are not a multiple of the 21 beacons per wave."""
+    import random
+    from oracle import bls12381 as O
+    rng = random.Random(5)
+    for n in (1, 21, 22, 100):
+        f = []
+        for _ in range(n):
+            for _ in range(12):
+                f += limbs(rng.randrange(O.P))
+        got, ref = engine.test_final_exp(f)
+        assert got == ref, n
+    # the identity stays the identity
+    one = [0] * 144
+    one[0] = 1
+    got, ref = engine.test_final_exp(one)
+    assert got == ref == one
