@@ -104,7 +104,9 @@ static int ensure_workspace(blsv_ctx* c, size_t cnt) {
   HIPCHK(c, c->S.ensure(want * blsk::S_WORDS * 4));
   HIPCHK(c, c->F.ensure(want * blsk::F_WORDS * 4));
   HIPCHK(c, c->FW.ensure(3 * want * blsk::F_WORDS * 4));
-  HIPCHK(c, c->LN.ensure(std::min(want, kLineSub) * blsk::MILLER_LINE_WORDS * 4));
+  HIPCHK(c, c->LN.ensure(std::max(std::min(want, kLineSub) * blsk::MILLER_LINE_WORDS,
+                                   blsk::TRI_PARK_WORDS(want)) * 4));  // LN doubles as the 3-lane park
+  static_assert(3 * blsk::F_WORDS >= 48 * 64 / 21 + 1, "FW holds the Miller park of a sub-chunk");
   HIPCHK(c, c->h_inf.ensure(want));
   HIPCHK(c, c->s_inf.ensure(want));
   HIPCHK(c, c->cls.ensure(want));
@@ -188,11 +190,13 @@ static int run_tail(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t of
     StageTimer tm(c, ST_MILLER, cnt, st);
     blsk::launch_miller(pk.tab, pk.inf, pk.idx, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->S.as<uint32_t>(),
                         c->s_inf.as<uint8_t>(), c->cls.as<uint8_t>(), cnt, c->F.as<uint32_t>(), c->LN.as<uint32_t>(),
-                        std::min(cnt, kLineSub), st);
+                        std::min(cnt, kLineSub), c->FW.as<uint32_t>(), st);
   }
   {
     StageTimer tm(c, ST_FEXP, cnt, st);
-    blsk::launch_final_exp(c->F.as<uint32_t>(), c->FW.as<uint32_t>(), cnt, c->cls.as<uint8_t>(), st);
+    // the 3-lane products park in LN (free after the Miller stage)
+    blsk::launch_final_exp(c->F.as<uint32_t>(), c->FW.as<uint32_t>(), cnt, c->cls.as<uint8_t>(), st,
+                           c->LN.as<uint32_t>());
   }
   {
     StageTimer tm(c, ST_FINISH, cnt, st);
@@ -880,7 +884,7 @@ int blsv_test_final_exp(blsv_ctx* c, const uint32_t* f, size_t n, uint32_t* out_
   blsk::launch_test_final_exp_ref(c->F.as<uint32_t>(), n, dref.as<uint32_t>(), c->stream);
   // the production stage (clobbers F), its final value captured into dout
   blsk::launch_final_exp(c->F.as<uint32_t>(), c->FW.as<uint32_t>(), n, c->cls.as<uint8_t>(), c->stream,
-                         dout.as<uint32_t>());
+                         c->LN.as<uint32_t>(), dout.as<uint32_t>());
   blsk::launch_test_unpack_fp12(dout.as<uint32_t>(), n, din.as<uint32_t>(), c->stream);
   HIPCHK(c, hipMemcpyAsync(out_pipeline, din.p, n * 576, hipMemcpyDeviceToHost, c->stream));
   blsk::launch_test_unpack_fp12(dref.as<uint32_t>(), n, dout.as<uint32_t>(), c->stream);

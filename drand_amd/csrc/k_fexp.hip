@@ -40,8 +40,14 @@ BLS_KERNEL(BLS_WPE_FEXP) k_fexp_step(const uint32_t* X, const uint32_t* C, const
 #define BLS_WPE_FEXP_TRI 2
 #endif
 
+// Park slot of the staged products (tri.h tri_mul_lp): 48 words per lane of the grid.
+struct TriPark {
+  uint32_t* p;
+  size_t n, i;
+};
+
 template <typename LoadX>
-DI fp4 tri_pow_x_abs(const tri_lane& t, LoadX lx) {
+DI fp4 tri_pow_x_abs(const tri_lane& t, LoadX lx, const TriPark& pk) {
   constexpr uint64_t NSQ = 1ull | (2ull << 6) | (3ull << 12) | (9ull << 18) | (32ull << 24) | (16ull << 30);
   fp4 r = lx();
 #pragma unroll 1
@@ -49,33 +55,34 @@ DI fp4 tri_pow_x_abs(const tri_lane& t, LoadX lx) {
     const int n = (int)((NSQ >> (6 * s)) & 63u);
 #pragma unroll 1
     for (int k = 0; k < n; k++) r = tri_cyclotomic_sqr(t, r);
-    if (s < 5) r = tri_mul(t, r, lx());
+    if (s < 5) r = tri_mul_lp(t, r, lx(), pk.p, pk.n, pk.i);
   }
   return r;
 }
 
 template <int MODE>
 BLS_KERNEL(BLS_WPE_FEXP_TRI) k_fexp_tri(const uint32_t* X, const uint32_t* C, const uint32_t* G, size_t cnt,
-                                        uint8_t* cls, uint32_t* OUT) {
+                                        uint8_t* cls, uint32_t* OUT, uint32_t* park) {
   const tri_lane t = tri_lane_id();
   const size_t ir = (size_t)blockIdx.x * TRI_GROUPS + t.group;
   const bool in_range = t.group < TRI_GROUPS && ir < cnt;
   const size_t i0 = in_range ? ir : cnt - 1;  // dummy lanes compute on a real row, never store
   const bool live = in_range && cls[i0] == REJ_OK;
+  const TriPark pk = {park, (size_t)gridDim.x * TPB, (size_t)blockIdx.x * TPB + t.lane};
   // every lane stays active to the end (ds_bpermute reads its partners' registers)
   auto at = [&](const uint32_t* B) {
     size_t j = i0;
     asm volatile("" : "+v"(j));  // re-read at each use, never hoisted (as in k_fexp_step)
     return tri_load(B, cnt, j, t.role);
   };
-  fp4 r = tri_conj(t, tri_pow_x_abs(t, [&]() { return at(X); }));
-  if (MODE == 0 || MODE == 1) r = tri_mul(t, r, tri_conj(t, at(X)));
-  if (MODE == 2) r = tri_mul(t, r, tri_frob(t, at(X)));
+  fp4 r = tri_conj(t, tri_pow_x_abs(t, [&]() { return at(X); }, pk));
+  if (MODE == 0 || MODE == 1) r = tri_mul_lp(t, r, tri_conj(t, at(X)), pk.p, pk.n, pk.i);
+  if (MODE == 2) r = tri_mul_lp(t, r, tri_frob(t, at(X)), pk.p, pk.n, pk.i);
   if (MODE == 4) {
-    r = tri_mul(t, r, tri_frob2(t, at(C)));
-    r = tri_mul(t, r, tri_conj(t, at(C)));
-    r = tri_mul(t, r, tri_cyclotomic_sqr(t, at(G)));
-    r = tri_mul(t, r, at(G));
+    r = tri_mul_lp(t, r, tri_frob2(t, at(C)), pk.p, pk.n, pk.i);
+    r = tri_mul_lp(t, r, tri_conj(t, at(C)), pk.p, pk.n, pk.i);
+    r = tri_mul_lp(t, r, tri_cyclotomic_sqr(t, at(G)), pk.p, pk.n, pk.i);
+    r = tri_mul_lp(t, r, at(G), pk.p, pk.n, pk.i);
   }
   if (MODE < 4 || OUT) {  // MODE 4 with OUT: the final value too (blsv_test_final_exp)
     if (live) tri_store(OUT, cnt, i0, t.role, r);
@@ -89,7 +96,8 @@ BLS_KERNEL(BLS_WPE_FEXP_TRI) k_fexp_tri(const uint32_t* X, const uint32_t* C, co
 // ------------------------------------------------------------------ launchers
 // F (Miller output) is consumed by the easy part and then reused as scratch; W holds 3 more Fp12
 // staging slots of cnt entries each (G, B, C).
-void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st, uint32_t* out) {
+void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st, uint32_t* park,
+                      uint32_t* out) {
   if (!cnt) return;
   uint32_t* G = W;
   uint32_t* B = W + cnt * F_WORDS;
@@ -103,13 +111,14 @@ void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStr
   hipLaunchKernelGGL(k_fexp_step<3>, grid, blk, 0, st, C, nullptr, nullptr, cnt, cls, F);  // t -> F
   hipLaunchKernelGGL(k_fexp_step<4>, grid, blk, 0, st, F, C, G, cnt, cls, nullptr);
   (void)out;
+  (void)park;
 #else
   const dim3 tgrid((unsigned)((cnt + TRI_GROUPS - 1) / TRI_GROUPS));
-  hipLaunchKernelGGL(k_fexp_tri<0>, tgrid, blk, 0, st, G, nullptr, nullptr, cnt, cls, F);  // a -> F
-  hipLaunchKernelGGL(k_fexp_tri<1>, tgrid, blk, 0, st, F, nullptr, nullptr, cnt, cls, B);  // b -> B
-  hipLaunchKernelGGL(k_fexp_tri<2>, tgrid, blk, 0, st, B, nullptr, nullptr, cnt, cls, C);  // c -> C
-  hipLaunchKernelGGL(k_fexp_tri<3>, tgrid, blk, 0, st, C, nullptr, nullptr, cnt, cls, F);  // t -> F
-  hipLaunchKernelGGL(k_fexp_tri<4>, tgrid, blk, 0, st, F, C, G, cnt, cls, out);
+  hipLaunchKernelGGL(k_fexp_tri<0>, tgrid, blk, 0, st, G, nullptr, nullptr, cnt, cls, F, park);  // a -> F
+  hipLaunchKernelGGL(k_fexp_tri<1>, tgrid, blk, 0, st, F, nullptr, nullptr, cnt, cls, B, park);  // b -> B
+  hipLaunchKernelGGL(k_fexp_tri<2>, tgrid, blk, 0, st, B, nullptr, nullptr, cnt, cls, C, park);  // c -> C
+  hipLaunchKernelGGL(k_fexp_tri<3>, tgrid, blk, 0, st, C, nullptr, nullptr, cnt, cls, F, park);  // t -> F
+  hipLaunchKernelGGL(k_fexp_tri<4>, tgrid, blk, 0, st, F, C, G, cnt, cls, out, park);
 #endif
 }
 

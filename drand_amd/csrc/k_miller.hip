@@ -66,17 +66,78 @@ BLS_KERNEL(BLS_WPE_MILLER_F) k_miller_f(const uint32_t* LN, const uint8_t* cls, 
   st_fp12(F, cnt, g, miller_f_from_lines(load));
 }
 
+// ------------------------------------------------------------------ 3-lane f pass (tri.h)
+// Same f as k_miller_f, each Fp12 spread over 3 lanes (Fp4 thirds), 21 beacons per wave: per step
+// f = f^2 (tri_sqr_lp), L = l_0 l_1 (tri_line_pair: 2 Fp2 products per lane), f = f L (tri_mul_lp).
+// Steps s = 0..67 follow miller_f_from_lines; bit s of MILLER_SQ says whether step s squares first.
+constexpr uint64_t miller_sq_bits(int half) {
+  uint64_t m = 0;
+  int s = 0;
+  for (int i = 62; i >= 0; i--) {
+    if (i != 62 && s / 64 == half) m |= 1ull << (s % 64);
+    s++;
+    if ((BLS_X_ABS >> i) & 1ull) s++;  // addition step: no squaring
+  }
+  return m;
+}
+constexpr uint64_t MILLER_SQ_LO = miller_sq_bits(0), MILLER_SQ_HI = miller_sq_bits(1);
+
+#ifndef BLS_WPE_MILLER_TRI
+#define BLS_WPE_MILLER_TRI 2
+#endif
+
+BLS_KERNEL(BLS_WPE_MILLER_TRI) k_miller_f_tri(const uint32_t* LN, const uint8_t* cls, size_t cnt, size_t base,
+                                              size_t m, size_t sub, uint32_t* F, uint32_t* park) {
+  const tri_lane t = tri_lane_id();
+  const size_t ir = (size_t)blockIdx.x * TRI_GROUPS + t.group;
+  const bool in_range = t.group < TRI_GROUPS && ir < m;
+  const size_t i = in_range ? ir : m - 1;  // dummy lanes compute on a real row, never store
+  const bool live = in_range && cls[base + i] == REJ_OK;
+  const size_t park_n = (size_t)gridDim.x * TPB, park_i = (size_t)blockIdx.x * TPB + t.lane;
+  fp4 A;
+#pragma unroll 1
+  for (int s = 0; s < MILLER_STEPS; s++) {
+    const bool sq = ((s < 64 ? MILLER_SQ_LO >> s : MILLER_SQ_HI >> (s - 64)) & 1ull) != 0;
+    if (sq) A = tri_sqr_lp(t, A);
+    const int s0 = line_slot(s, 0), s1 = line_slot(s, 1);
+    auto la = [&](int c) {
+      size_t j = i;
+      asm volatile("" : "+v"(j));
+      return ld_fp2(LN, sub, j, s0 + 2 * c);
+    };
+    auto lb = [&](int c) {
+      size_t j = i;
+      asm volatile("" : "+v"(j));
+      return ld_fp2(LN, sub, j, s1 + 2 * c);
+    };
+    const fp4 L = tri_line_pair(t, la, lb);
+    if (s == 0) {
+      A = L;  // f = 1 * L
+    } else {
+      A = tri_mul_lp(t, A, L, park, park_n, park_i);
+    }
+  }
+  A = tri_conj(t, A);
+  if (live) tri_store(F, cnt, base + i, t.role, A);
+}
+
 // ------------------------------------------------------------------ launchers
 // The line staging (MILLER_LINE_WORDS per beacon) holds `sub` beacons; the chunk runs in sub-chunks.
 void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
                    const uint8_t* h_inf, const uint32_t* S, const uint8_t* s_inf, const uint8_t* cls, size_t cnt,
-                   uint32_t* F, uint32_t* LN, size_t sub, hipStream_t st) {
+                   uint32_t* F, uint32_t* LN, size_t sub, uint32_t* park, hipStream_t st) {
   if (!cnt) return;
   for (size_t b = 0; b < cnt; b += sub) {
     const size_t m = cnt - b < sub ? cnt - b : sub;
     hipLaunchKernelGGL(k_miller_lines, dim3(grid_for(m)), dim3(TPB), 0, st, pk_tab, pk_inf, pk_idx, H, h_inf, S,
                        s_inf, cls, cnt, b, m, sub, LN);
+#ifdef BLS_MILLER_TRI
+    hipLaunchKernelGGL(k_miller_f_tri, dim3((unsigned)((m + TRI_GROUPS - 1) / TRI_GROUPS)), dim3(TPB), 0, st, LN, cls,
+                       cnt, b, m, sub, F, park);
+#else
     hipLaunchKernelGGL(k_miller_f, dim3(grid_for(m)), dim3(TPB), 0, st, LN, cls, cnt, b, m, sub, F);
+    (void)park;
+#endif
   }
 }
 

@@ -48,10 +48,14 @@ void launch_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, siz
 constexpr int MILLER_LINE_WORDS = 68 * 2 * 6 * 12;
 void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
                    const uint8_t* h_inf, const uint32_t* S, const uint8_t* s_inf, const uint8_t* cls, size_t cnt,
-                   uint32_t* F, uint32_t* LN, size_t sub, hipStream_t st);
+                   uint32_t* F, uint32_t* LN, size_t sub, uint32_t* park, hipStream_t st);
+// park: TRI_PARK_WORDS(sub) words of scratch for the 3-lane f pass (48 words per lane, 21 items per wave)
+constexpr size_t TRI_PARK_WORDS(size_t items) { return 48 * 64 * ((items + 20) / 21); }
 // F is clobbered; W = 3 * cnt * F_WORDS words of staging; out (optional, test hook): the
 // exponentiated values (SoA, cnt * F_WORDS words)
-void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st, uint32_t* out = nullptr);
+// park: TRI_PARK_WORDS(cnt) words of scratch for the 3-lane products
+void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st, uint32_t* park,
+                      uint32_t* out = nullptr);
 // bitmap bit (base+i) = (cls[i] == 0); bitmap must cover whole 64-bit words;
 // first_bad = label0 + min rejected index (label0 = first_round -> ROUND numbers)
 void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap, unsigned long long* first_bad,

@@ -157,13 +157,206 @@ DI fp4 tri_sqr(const tri_lane& t, const fp4& a) {
   return fp4_select(t.role == 0, k0, fp4_select(t.role == 1, k1, k2));
 }
 
+// ------------------------------------------------------------------ low register pressure products
+// A called fp2 product clobbers every caller-saved VGPR, so whatever the caller keeps live across the
+// call must sit in the callee-saved half of the file (112 VGPRs at a 256-VGPR budget) or be spilled
+// around each call. The Miller f pass therefore stages its second operands in LDS: each lane owns a
+// 72-word column (3 Fp2 slots). A staged Fp4 y sits there as (y.a, y.b, y.a + y.b), and an Fp4
+// product x y keeps only x and its partial products in VGPRs across the three calls. 72 words x 64
+// lanes = 18 KB per one-wave workgroup: 8 workgroups (2 waves/SIMD) fit the CU's 160 KB.
+constexpr int TRI_ARG_WORDS = 72;
+static __shared__ uint32_t g_tri_arg[TRI_ARG_WORDS * BLS_LANES];
+
+DI void tri_arg_put(int slot, const fp2& v) {
+  const unsigned l = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    g_tri_arg[(slot * 24 + k) * BLS_LANES + l] = v.c0.l[k];
+    g_tri_arg[(slot * 24 + 12 + k) * BLS_LANES + l] = v.c1.l[k];
+  }
+}
+DI fp2 tri_arg_get(int slot) {
+  const unsigned l = threadIdx.x;
+  fp2 v;
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    v.c0.l[k] = g_tri_arg[(slot * 24 + k) * BLS_LANES + l];
+    v.c1.l[k] = g_tri_arg[(slot * 24 + 12 + k) * BLS_LANES + l];
+  }
+  return v;
+}
+
+// LDS slot layout per lane: slot 0 = y.a, slot 1 = y.b, slot 2 = the product's result. The callee
+// reads b = slot 0, slot 1, or their lazy sum (sel 2), and writes a * b to slot 2: neither b nor the
+// result travels in registers (a returned 24-word vector is spilled whole around the call site).
+NOINL void fp2_mul_slot_u24(u24 a, int sel) {
+  const unsigned l = threadIdx.x;
+  u12 b0, b1;
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    const uint32_t p0 = g_tri_arg[k * BLS_LANES + l], p1 = g_tri_arg[(12 + k) * BLS_LANES + l];
+    const uint32_t q0 = g_tri_arg[(24 + k) * BLS_LANES + l], q1 = g_tri_arg[(36 + k) * BLS_LANES + l];
+    b0[k] = sel == 0 ? p0 : q0;
+    b1[k] = sel == 0 ? p1 : q1;
+  }
+  if (sel == 2) {  // y.a + y.b (< 2p each: the sum stays below 4p, fp.h operand contract)
+    u12 a0, a1;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      a0[k] = g_tri_arg[k * BLS_LANES + l];
+      a1[k] = g_tri_arg[(12 + k) * BLS_LANES + l];
+    }
+    b0 = fp_add_raw_u12(b0, a0);
+    b1 = fp_add_raw_u12(b1, a1);
+  }
+  const u24 r = fp2_mul_body(a, b0, b1);
+#pragma unroll
+  for (int k = 0; k < 24; k++) g_tri_arg[(48 + k) * BLS_LANES + l] = r[k];
+}
+// The argument vector is rebuilt from opaque words at every call: a CSE'd 24-word argument vector
+// live across later calls would be spilled whole (as a 32-register tuple).
+DI u24 fp2_to_u24_fresh(const fp2& a) {
+  fp2 c = a;
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    asm volatile("" : "+v"(c.c0.l[k]));
+    asm volatile("" : "+v"(c.c1.l[k]));
+  }
+  return fp2_to_u24(c);
+}
+DI fp2 fp2_mul_slot(const fp2& a, int sel) {
+  fp2_mul_slot_u24(fp2_to_u24_fresh(a), sel);
+  return tri_arg_get(2);
+}
+// a^2 into slot 2 (slots 0, 1 untouched)
+NOINL void fp2_sqr_slot_u24(u24 a) {
+  const unsigned l = threadIdx.x;
+  const u24 r = fp2_sqr_body(a);
+#pragma unroll
+  for (int k = 0; k < 24; k++) g_tri_arg[(48 + k) * BLS_LANES + l] = r[k];
+}
+DI fp2 fp2_sqr_slot(const fp2& a) {
+  fp2_sqr_slot_u24(fp2_to_u24_fresh(a));
+  return tri_arg_get(2);
+}
+DI fp4 fp4_sqr_slot(const fp4& x) {
+  const fp2 t0 = fp2_sqr_slot(x.a);
+  const fp2 t1 = fp2_sqr_slot(x.b);
+  const fp2 t2 = fp2_sqr_slot(fp2_add_lazy(x.a, x.b));
+  return {fp2_add(t0, fp2_mul_xi(t1)), fp2_sub(fp2_sub(t2, t0), t1)};
+}
+DI fp4 fp4_neg(const fp4& x) { return {fp2_neg(x.a), fp2_neg(x.b)}; }
+
+// one product: b through slot 0
+DI fp2 fp2_mul_staged1(const fp2& a, const fp2& b) {
+  tri_arg_put(0, b);
+  return fp2_mul_slot(a, 0);
+}
+DI void fp4_stage(const fp4& y) {
+  tri_arg_put(0, y.a);
+  tri_arg_put(1, y.b);
+}
+// x * (staged y), Karatsuba over s as fp4_mul
+DI fp4 fp4_mul_staged(const fp4& x) {
+  const fp2 t0 = fp2_mul_slot(x.a, 0);
+  const fp2 t1 = fp2_mul_slot(x.b, 1);
+  const fp2 t2 = fp2_mul_slot(fp2_add_lazy(x.a, x.b), 2);
+  return {fp2_add(t0, fp2_mul_xi(t1)), fp2_sub(fp2_sub(t2, t0), t1)};
+}
+
+// tri_sqr with at most one Fp4 plus partial products live at any call: M is exchanged and parked in
+// LDS while the squares run.
+DI fp4 tri_sqr_lp(const tri_lane& t, const fp4& a) {
+  const int self_b = (int)(4u * t.lane);
+  fp4_stage(xchg_fp4(a, t.next_b));
+  const fp4 M = fp4_mul_staged(a);                                                   // M_j = A_j A_{j+1}
+  const fp4 Mx = xchg_fp4(M, t.role == 0 ? t.next_b : (t.role == 1 ? t.prev_b : self_b));  // r0: M1 r1: M0 r2: M2
+  tri_arg_put(0, Mx.a);
+  tri_arg_put(1, Mx.b);
+  const fp4 S = fp4_sqr_slot(a);                                                      // S_j = A_j^2
+  const fp4 Sx = xchg_fp4(S, t.role == 1 ? t.next_b : (t.role == 2 ? t.prev_b : self_b));  // r0: S0 r1: S2 r2: S1
+  // r0: S0 + s 2 M1,  r1: 2 M0 + s S2,  r2: S1 + 2 M2
+  const fp4 U = fp4_select(t.role == 1, fp4_mul_s(Sx), Sx);
+  const fp4 D = fp4_dbl(fp4{tri_arg_get(0), tri_arg_get(1)});
+  return fp4_add(U, fp4_select(t.role == 0, fp4_mul_s(D), D));
+}
+
+// This lane's third of L = l_0 l_1, the product of the two pairs' sparse lines of one Miller step
+// (pairing.h line_mul_line; L.c1.c0 = 0), with two Fp2 products per lane:
+//   r0: X = t00, Y = t44;  r1: X = t11, Y = K01;  r2: X = K04, Y = K14
+// (t_kk = a_k b_k, K_jk = (a_j + a_k)(b_j + b_k); a = pair 0's line, b = pair 1's; components 0, 1, 2 =
+// the line's a0, a1, a4). la(c) / lb(c) load component c of the two lines.
+template <typename LoadA, typename LoadB>
+DI fp4 tri_line_pair(const tri_lane& t, LoadA la, LoadB lb) {
+  const unsigned r = t.role;
+  const int xc = r == 1 ? 1 : 0;
+  fp2 xa = la(xc), xb = lb(xc);
+  if (r == 2) {
+    xa = fp2_add_lazy(xa, la(2));
+    xb = fp2_add_lazy(xb, lb(2));
+  }
+  const fp2 X = fp2_mul_staged1(xa, xb);
+  const int yc = r == 0 ? 2 : (r == 1 ? 0 : 1);
+  fp2 ya = la(yc), yb = lb(yc);
+  if (r != 0) {
+    const int yc2 = r == 1 ? 1 : 2;
+    ya = fp2_add_lazy(ya, la(yc2));
+    yb = fp2_add_lazy(yb, lb(yc2));
+  }
+  const fp2 Y = fp2_mul_staged1(ya, yb);
+  const fp2 Xp = xchg_fp2(X, t.prev_b), Yp = xchg_fp2(Y, t.prev_b);
+  const fp2 Xn = xchg_fp2(X, t.next_b), Yn = xchg_fp2(Y, t.next_b);
+  // r0: (t00 + xi t44, K04 - t00 - t44)   r1: (0, t11)   r2: (K01 - t00 - t11, K14 - t11 - t44)
+  const fp2 a0 = fp2_add(X, fp2_mul_xi(Y)), b0 = fp2_sub(fp2_sub(Xp, X), Y);
+  const fp2 a2 = fp2_sub(fp2_sub(Yp, Xn), Xp), b2 = fp2_sub(fp2_sub(Y, Xp), Yn);
+  return {fp2_select(r == 0, a0, fp2_select(r == 1, fp2_zero(), a2)), fp2_select(r == 0, b0, fp2_select(r == 1, X, b2))};
+}
+
+// tri_mul(a, b) with b staged in LDS; the partial result from P parks in `park` (a per-lane global
+// SoA slot of 48 words: word w at park[w * park_n + park_i]) while Q is formed.
+DI fp4 tri_mul_lp(const tri_lane& t, const fp4& a, const fp4& b, uint32_t* park, size_t park_n, size_t park_i) {
+  const int self_b = (int)(4u * t.lane);
+  fp4_stage(b);
+  const fp4 P = fp4_mul_staged(a);  // P_j = A_j B_j
+  {
+    const fp4 br = {tri_arg_get(0), tri_arg_get(1)};
+    fp4_stage(fp4_add_lazy(br, xchg_fp4(br, t.next_b)));  // B_j + B_{j+1}
+  }
+  // partial results without Q:  r0: P - s (Pn + Pp),  r1: s Pn - Pp - P,  r2: Pp - P - Pn, built one
+  // exchanged term at a time (fewer Fp4 values live)
+  fp4 R = fp4_select(t.role == 0, P, fp4_neg(P));
+  {
+    const fp4 Pn = xchg_fp4(P, t.next_b);
+    const fp4 u = fp4_select(t.role == 2, Pn, fp4_mul_s(Pn));
+    R = fp4_add(R, fp4_select(t.role == 1, u, fp4_neg(u)));
+  }
+  {
+    const fp4 Pp = xchg_fp4(P, t.prev_b);
+    const fp4 u = fp4_select(t.role == 0, fp4_mul_s(Pp), Pp);
+    R = fp4_add(R, fp4_select(t.role == 2, u, fp4_neg(u)));
+  }
+  {
+    size_t j = park_i;
+    asm volatile("" : "+v"(j));  // park addresses are formed here, not hoisted out of the Miller loop
+    st_fp2(park, park_n, j, 0, R.a);
+    st_fp2(park, park_n, j, 2, R.b);
+  }
+  const fp4 Q = fp4_mul_staged(fp4_add_lazy(a, xchg_fp4(a, t.next_b)));  // Q_j
+  const fp4 Qx = xchg_fp4(Q, t.role == 0 ? t.next_b : (t.role == 1 ? t.prev_b : self_b));  // r0: Q1 r1: Q0 r2: Q2
+  size_t j = park_i;
+  asm volatile("" : "+v"(j));  // the park reload stays here
+  const fp4 Rp = {ld_fp2(park, park_n, j, 0), ld_fp2(park, park_n, j, 2)};
+  // r0: R + s Q1,  r1: R + Q0,  r2: R + Q2
+  return fp4_add(Rp, fp4_select(t.role == 0, fp4_mul_s(Qx), Qx));
+}
+
 // Frobenius f^p: c_k -> conj(c_k) gamma1^k; lane j holds c_j, c_{j+3}
 DI fp4 tri_frob(const tri_lane& t, const fp4& x) {
   const int j = (int)t.role;
   fp2 ga = fp2_load_const(FROB1_GAMMA[0]), gb = fp2_load_const(FROB1_GAMMA[3]);
   ga = fp2_select(j == 1, fp2_load_const(FROB1_GAMMA[1]), fp2_select(j == 2, fp2_load_const(FROB1_GAMMA[2]), ga));
   gb = fp2_select(j == 1, fp2_load_const(FROB1_GAMMA[4]), fp2_select(j == 2, fp2_load_const(FROB1_GAMMA[5]), gb));
-  return {fp2_mul(fp2_conj(x.a), ga), fp2_mul(fp2_conj(x.b), gb)};
+  return {fp2_mul_staged1(fp2_conj(x.a), ga), fp2_mul_staged1(fp2_conj(x.b), gb)};
 }
 
 // f^(p^2): c_k -> c_k gamma2^k (gamma2^k in Fp)
