@@ -82,6 +82,11 @@ constexpr uint64_t miller_sq_bits(int half) {
 }
 constexpr uint64_t MILLER_SQ_LO = miller_sq_bits(0), MILLER_SQ_HI = miller_sq_bits(1);
 
+#ifndef BLS_MILLER_TRI_MAX
+#define BLS_MILLER_TRI_MAX 65536
+#endif
+constexpr size_t kMillerTriMax = BLS_MILLER_TRI_MAX;
+
 #ifndef BLS_WPE_MILLER_TRI
 #define BLS_WPE_MILLER_TRI 2
 #endif
@@ -131,13 +136,15 @@ void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t
     const size_t m = cnt - b < sub ? cnt - b : sub;
     hipLaunchKernelGGL(k_miller_lines, dim3(grid_for(m)), dim3(TPB), 0, st, pk_tab, pk_inf, pk_idx, H, h_inf, S,
                        s_inf, cls, cnt, b, m, sub, LN);
-#ifdef BLS_MILLER_TRI
-    hipLaunchKernelGGL(k_miller_f_tri, dim3((unsigned)((m + TRI_GROUPS - 1) / TRI_GROUPS)), dim3(TPB), 0, st, LN, cls,
-                       cnt, b, m, sub, F, park);
-#else
-    hipLaunchKernelGGL(k_miller_f, dim3(grid_for(m)), dim3(TPB), 0, st, LN, cls, cnt, b, m, sub, F);
-    (void)park;
-#endif
+    // Below one full wave round of the single-lane pass (1 wave/SIMD x 1024 SIMDs x 64 lanes) the GPU is
+    // not full and latency decides: the 3-lane pass runs 27.6 k instructions per lane-step against
+    // 73.7 k. At full occupancy the single-lane pass has the higher throughput (profiles/r02_*).
+    if (m <= kMillerTriMax) {
+      hipLaunchKernelGGL(k_miller_f_tri, dim3((unsigned)((m + TRI_GROUPS - 1) / TRI_GROUPS)), dim3(TPB), 0, st, LN,
+                         cls, cnt, b, m, sub, F, park);
+    } else {
+      hipLaunchKernelGGL(k_miller_f, dim3(grid_for(m)), dim3(TPB), 0, st, LN, cls, cnt, b, m, sub, F);
+    }
   }
 }
 

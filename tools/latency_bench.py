@@ -1,0 +1,102 @@
+"""Latency of the per-arrival callers on one MI355X:
+
+  lone VerifyRecovered  (chain.VerifyBeacon of one beacon, node.go / validator.go arrival path)
+  lone VerifyPartial    (one partial of a round, chain/beacon/node.go:112,125)
+  64 VerifyPartial      (one round's partials in one call)
+  aggregator round      (blsv_aggregate: 64 partials, Recover from 33, VerifyRecovered)
+
+Each is the median wall clock over `reps` calls from the host API, plus the per-stage GPU time of
+one call (HIP events on the launch stream, blsv_profile_*). Inputs are the committed golden vectors
+(tests/golden/golden.json); every result is checked against them.
+
+usage: python tools/latency_bench.py [--reps 20] [--out profiles/r02_latency.json]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def timed(fn, reps):
+    lat = []
+    for k in range(reps + 2):
+        t0 = time.perf_counter()
+        fn()
+        dt = (time.perf_counter() - t0) * 1e3
+        if k >= 2:
+            lat.append(dt)
+    return round(statistics.median(lat), 3), round(min(lat), 3)
+
+
+def stages(eng, fn):
+    eng.profile(True)
+    eng.profile_read()
+    fn()
+    eng.synchronize()
+    got = eng.profile_read()
+    eng.profile(False)
+    return {k: round(v[0], 3) for k, v in got.items() if v[1]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    from drand_amd.engine import Engine
+
+    with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+        g = json.load(f)
+    ch, th = g["chained"], g["threshold"]
+    sigs = [bytes.fromhex(b["sig"]) for b in ch["beacons"]]
+    seed = bytes.fromhex(ch["genesis_seed"])
+    commits = [bytes.fromhex(c) for c in th["commits"]]
+    msg = bytes.fromhex(th["msg"])
+    partials = [bytes.fromhex(p) for p in th["partials"]]
+    out = {}
+    with Engine(0) as eng:
+        eng.set_public_key(bytes.fromhex(ch["pk"]))
+
+        def lone_beacon():
+            r = eng.verify_chained(2, sigs[0], [sigs[1]])
+            assert r.ok == [True]
+
+        med, mn = timed(lone_beacon, a.reps)
+        out["lone_verify_beacon"] = {"median_ms": med, "min_ms": mn, "stages_ms": stages(eng, lone_beacon)}
+
+        eng.set_group(commits, th["n"])
+
+        def lone_partial():
+            ok, _ = eng.verify_partials(msg, partials[:1])
+            assert ok == [True]
+
+        med, mn = timed(lone_partial, a.reps)
+        out["lone_verify_partial"] = {"median_ms": med, "min_ms": mn, "stages_ms": stages(eng, lone_partial)}
+
+        def round_partials():
+            ok, _ = eng.verify_partials(msg, partials)
+            assert all(ok)
+
+        med, mn = timed(round_partials, a.reps)
+        out["verify_partials_64"] = {"median_ms": med, "min_ms": mn, "stages_ms": stages(eng, round_partials)}
+
+        def agg():
+            ok, _, sig, gok = eng.aggregate(msg, partials, th["t"], th["n"])
+            assert all(ok) and gok and sig.hex() == th["group_sig"]
+
+        med, mn = timed(agg, a.reps)
+        out["aggregate_round_n64_t33"] = {"median_ms": med, "min_ms": mn, "stages_ms": stages(eng, agg)}
+    line = json.dumps(out)
+    print(line)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
+
+
+if __name__ == "__main__":
+    main()
