@@ -54,7 +54,9 @@ def test_wrong_length_rejected_host_side(engine, golden):
         engine.verify_unchained([b""], first_round=1)
 
 
-def test_infinity_rules_match_oracle(engine, golden):
+def test_infinity_rules_parity_unpinned(engine, golden):
+    """PARITY UNPINNED: kilic's treatment of points at infinity in the pairing product (a pair with an
+    infinity point is skipped), restated from its published source; no reference fixture."""
     kat = golden["kat"]
     msg = bytes.fromhex(kat["msg"])
     sig = bytes.fromhex(kat["sig"])
@@ -68,7 +70,9 @@ def test_infinity_rules_match_oracle(engine, golden):
         assert res.reject_class == [want], (pk48[:1].hex(), s[:1].hex())
 
 
-def test_recover_selection_rules(engine, golden):
+def test_recover_selection_rules_dedup_parity_unpinned(engine, golden):
+    """Any t valid shares give the group signature (pinned by the threshold fixture); the duplicate-
+    index rule at the end is PARITY UNPINNED (kyber's published Recover/xyCommit, no reference test)."""
     th = golden["threshold"]
     engine.set_group([bytes.fromhex(c) for c in th["commits"]], th["n"])
     msg = bytes.fromhex(th["msg"])
