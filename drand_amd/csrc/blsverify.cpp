@@ -75,6 +75,7 @@ struct blsv_ctx {
   // staging workspace
   size_t cap = 0;
   DBuf H, S, F, FW, LN, h_inf, s_inf, cls;
+  DBuf HQ;  // hash-to-G2 phase staging (kernels.h HQ_WORDS per item)
   // inputs / outputs
   DBuf in_sigs, in_msgs, in_off, in_len, in_rounds, seeds, bitmap, first_bad, sk, idx, lambdas, scratch, out,
       pp_tab, pp_inf, sel, g1_cls, misc;
@@ -101,6 +102,7 @@ static int ensure_workspace(blsv_ctx* c, size_t cnt) {
   want = (want + 63) & ~size_t(63);
   if (want <= c->cap) return BLSV_OK;
   HIPCHK(c, c->H.ensure(want * blsk::H_WORDS * 4));
+  HIPCHK(c, c->HQ.ensure(want * blsk::HQ_WORDS * 4));
   HIPCHK(c, c->S.ensure(want * blsk::S_WORDS * 4));
   HIPCHK(c, c->F.ensure(want * blsk::F_WORDS * 4));
   HIPCHK(c, c->FW.ensure(3 * want * blsk::F_WORDS * 4));
@@ -383,7 +385,7 @@ int blsv_verify_chained(blsv_ctx* c, uint64_t first_round, const uint8_t* prev0,
   int rc = verify_driver(
       c, n, c->in_sigs.as<uint8_t>(), 96, 0, group_pk(c),
       [&](size_t base, size_t cnt) {
-        blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
+        blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
       },
       ok_bitmap, &fb, reject_class);
   if (rc) return rc;
@@ -411,7 +413,7 @@ int blsv_verify_prevs(blsv_ctx* c, uint64_t first_round, const uint8_t* prevs96,
   int rc = verify_driver(
       c, n, c->in_sigs.as<uint8_t>(), 96, 0, group_pk(c),
       [&](size_t base, size_t cnt) {
-        blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
+        blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
       },
       ok_bitmap, &fb, reject_class);
   if (rc) return rc;
@@ -438,7 +440,7 @@ int blsv_verify_unchained(blsv_ctx* c, const uint64_t* rounds, uint64_t first_ro
       c, n, c->in_sigs.as<uint8_t>(), 96, 0, group_pk(c),
       [&](size_t base, size_t cnt) {
         blsk::launch_hash_unchained(d_rounds, first_round, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(),
-                                    c->stream);
+                                    c->HQ.as<uint32_t>(), c->stream);
       },
       ok_bitmap, &fb, reject_class);
   if (rc) return rc;
@@ -476,7 +478,7 @@ int blsv_verify_messages(blsv_ctx* c, const uint8_t* pk48, const uint8_t* msgs, 
       [&](size_t base, size_t cnt) {
         blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>() + base,
                                    c->in_len.as<uint32_t>() + base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(),
-                                   c->stream);
+                                   c->HQ.as<uint32_t>(), c->stream);
       },
       ok_bitmap, first_bad, reject_class);
 }
@@ -515,7 +517,7 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
   }
   if (rc) return rc;
   blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), k,
-                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
+                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
   HIPCHK(c, c->idx.ensure(k * 4));
   HIPCHK(c, hipMemcpyAsync(c->idx.p, index.data(), k * 4, hipMemcpyHostToDevice, c->stream));
   // PubPoly.Eval(index): the per-group table when every index is a member index (< n), else
@@ -746,7 +748,7 @@ int blsv_sign(blsv_ctx* c, const uint8_t* sk32, int32_t index, const uint8_t* ms
   HIPCHK(c, c->out.ensure(n * stride));
   HIPCHK(c, hipMemcpyAsync(c->sk.p, sk, 32, hipMemcpyHostToDevice, c->stream));
   blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), n,
-                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
+                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
   blsk::launch_sign(c->sk.as<uint32_t>(), index, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), n, c->out.as<uint8_t>(),
                     stride, c->stream);
   HIPCHK(c, hipGetLastError());
@@ -775,7 +777,7 @@ int blsv_verify_chained_dev(blsv_ctx* c, uint64_t first_round, uint64_t seg_len,
     const size_t cnt = std::min(c->cap, n - base);
     {
       StageTimer tm(c, ST_HASH, cnt, st);
-      blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), st);
+      blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), st);
     }
     rc = run_tail(c, d_sigs96, 96, 0, base, cnt, group_pk(c), d_bitmap, (unsigned long long*)d_first_bad,
                   d_reject_class, st, first_round);  // d_first_bad holds a ROUND (include/blsverify.h)
@@ -906,7 +908,7 @@ int blsv_test_hash_to_g2(blsv_ctx* c, const uint8_t* msgs, const uint32_t* msg_l
   DBuf dout;
   HIPCHK(c, dout.ensure(n * 192));
   blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), n,
-                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->stream);
+                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
   blsk::launch_test_unpack_g2(c->H.as<uint32_t>(), n, dout.as<uint32_t>(), c->stream);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(out, dout.p, n * 192, hipMemcpyDeviceToHost, c->stream));

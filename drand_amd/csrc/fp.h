@@ -1,5 +1,8 @@
 // Fp arithmetic for BLS12-381 on gfx950: 381-bit prime field, 12 x 32-bit little-endian limbs,
-// Montgomery form (R = 2^392, see fp_mul_u12), values kept canonical in [0, p).
+// Montgomery form (R = 2^392, see fp_mul_u12). Values live in the redundant range [0, 2p): a
+// multiplier output needs no final subtraction (its bound is < 2p for ANY 12-word inputs, see the
+// operand contract above fp_mul_u12), and add/sub/neg keep [0, 2p) with one 2p correction. Only
+// comparisons (fp_is_zero, fp_eq) and leaving Montgomery form (fp_from_mont) canonicalise.
 //
 // This is the engine's replacement for kilic/bls12-381's fp.go + the amd64 assembly Montgomery
 // multiply (the [ext] native code on the reference path). Everything above this
@@ -52,18 +55,23 @@ DI fp fp_zero() {
 
 DI fp fp_one() { return fp_load_const(FP_ONE); }
 
-DI bool fp_is_zero(const fp& a) {
+// a == 0 as a 12-word integer (not mod p)
+DI bool fp_raw_is_zero(const fp& a) {
   uint32_t acc = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) acc |= a.l[i];
   return acc == 0;
 }
 
-DI bool fp_eq(const fp& a, const fp& b) {
-  uint32_t acc = 0;
+// a == 0 mod p for a in [0, 2p): a is 0 or p
+DI bool fp_is_zero(const fp& a) {
+  uint32_t z = 0, q = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) acc |= a.l[i] ^ b.l[i];
-  return acc == 0;
+  for (int i = 0; i < 12; i++) {
+    z |= a.l[i];
+    q |= a.l[i] ^ P_RAW[i];
+  }
+  return (z == 0) | (q == 0);
 }
 
 DI fp fp_select(bool c, const fp& a, const fp& b) {  // c ? a : b
@@ -73,17 +81,27 @@ DI fp fp_select(bool c, const fp& a, const fp& b) {  // c ? a : b
   return r;
 }
 
-// r = a - p if a >= p else a, for a < 2p (given as 12 limbs + carry word)
-DI fp fp_reduce_once(const uint32_t (&s)[12], uint32_t carry) {
+// r = s - 2p if s >= 2p else s, for s < 4p (< 2^383: no carry word)
+DI fp fp_reduce_2p(const uint32_t (&s)[12]) {
   uint32_t d[12];
   unsigned br = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(s[i], P_RAW[i], br, &br);
-  // keep s if (carry == 0 and borrow) i.e. s < p
-  bool keep = (carry == 0) & (br != 0);
+  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(s[i], P2_RAW[i], br, &br);
   fp r;
 #pragma unroll
-  for (int i = 0; i < 12; i++) r.l[i] = keep ? s[i] : d[i];
+  for (int i = 0; i < 12; i++) r.l[i] = br ? s[i] : d[i];
+  return r;
+}
+
+// canonical representative: a - p if a >= p, for a in [0, 2p)
+DI fp fp_canon(const fp& a) {
+  uint32_t d[12];
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(a.l[i], P_RAW[i], br, &br);
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = br ? a.l[i] : d[i];
   return r;
 }
 
@@ -92,13 +110,14 @@ DI fp fp_add(const fp& a, const fp& b) {
   unsigned c = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) s[i] = __builtin_addc(a.l[i], b.l[i], c, &c);
-  return fp_reduce_once(s, c);
+  return fp_reduce_2p(s);
 }
 
 DI fp fp_dbl(const fp& a) { return fp_add(a, a); }
 
 // a + b WITHOUT reduction, for inputs < 2p: the result (< 4p) may only feed a multiplier (see the
-// operand contract above fp_mul_u12), never fp_add/fp_sub/fp_eq or serialization.
+// operand contract above fp_mul_u12) or one more fp_add_lazy (< 8p, the most any multiplier operand
+// carries), never fp_add/fp_sub/fp_eq or serialization.
 DI fp fp_add_lazy(const fp& a, const fp& b) {
   fp r;
   unsigned c = 0;
@@ -107,7 +126,8 @@ DI fp fp_add_lazy(const fp& a, const fp& b) {
   return r;
 }
 
-// a/2 mod p: (a + (a odd ? p : 0)) >> 1 (the sum is < 2p < 2^382, no 13th limb needed)
+// a/2 mod p: (a + (a odd ? p : 0)) >> 1 (a < 2p: the sum is < 3p < 2^383, no 13th limb needed; the
+// result is < 1.5p)
 DI fp fp_half(const fp& a) {
   const uint32_t m = 0u - (a.l[0] & 1u);
   uint32_t s[12];
@@ -121,38 +141,45 @@ DI fp fp_half(const fp& a) {
   return r;
 }
 
+// a - b for a, b in [0, 2p): the difference is in (-2p, 2p); 2p is added back on a borrow
 DI fp fp_sub(const fp& a, const fp& b) {
   uint32_t d[12];
   unsigned br = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) d[i] = __builtin_subc(a.l[i], b.l[i], br, &br);
-  // if borrow, add p back
   uint32_t m = br ? 0xffffffffu : 0u;
   unsigned c = 0;
   fp r;
 #pragma unroll
-  for (int i = 0; i < 12; i++) r.l[i] = __builtin_addc(d[i], P_RAW[i] & m, c, &c);
+  for (int i = 0; i < 12; i++) r.l[i] = __builtin_addc(d[i], P2_RAW[i] & m, c, &c);
   return r;
 }
 
+// 2p - a, or 0 for a == 0 (keeps the result below 2p)
 DI fp fp_neg(const fp& a) {
   uint32_t d[12];
   unsigned br = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(P_RAW[i], a.l[i], br, &br);
-  uint32_t m = fp_is_zero(a) ? 0u : 0xffffffffu;
+  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(P2_RAW[i], a.l[i], br, &br);
+  uint32_t m = fp_raw_is_zero(a) ? 0u : 0xffffffffu;
   fp r;
 #pragma unroll
   for (int i = 0; i < 12; i++) r.l[i] = d[i] & m;
   return r;
 }
 
+// a == b mod p for a, b in [0, 2p)
+DI bool fp_eq(const fp& a, const fp& b) { return fp_is_zero(fp_sub(a, b)); }
+
 typedef uint32_t u12 __attribute__((ext_vector_type(12)));
 
 // Operand contract of the multipliers (fp_mul_u12, fp_sqr_u12, fp2_mul_u24, fp2_sqr_u24): every
-// input word-vector may be any value < 4p ("lazily reduced": the sum of two values < 2p, see
-// fp_add_lazy), outputs are canonical in [0, p). With inputs < 4p a Montgomery dot product of two
-// terms is < 2 * (8p)^2 = 128 p^2 < 2^769, so the result (< 2^377 + p) needs one subtraction.
+// input word-vector may be ANY 12-word value (< 2^384; in practice < 8p: at most two levels of lazily
+// added values < 2p, see fp_add_lazy). Inside the Fp2 bodies negations (16p - y) and sums of such
+// operands are formed limb-wise in radix 2^28 (limbs < 2^29.6, values < 2^386). The output is < 2p,
+// with no final subtraction: a Montgomery dot product of two terms is < 2 * 2^771, so the result
+// (T + m p) / R < 2^772 / 2^392 + p = 2^380 + p < 2p. Column sums stay < 2^63 (at most 28 limb
+// products < 2^58, or 14 < 2^58.6, plus 14 of m_j p_{k-j} < 2^56 and the carried-in column).
 // Montgomery product a*b*R^-1 mod p, R = 2^392.
 // Deliberately NOT inlined: one copy of the body per code object keeps kernels small
 // (instruction-cache resident) and compile times sane. Arguments/results are ext_vector u12 so
@@ -164,8 +191,8 @@ typedef uint32_t u12 __attribute__((ext_vector_type(12)));
 // 32-bit-limb form needs one v_addc per product): 588 VALU instructions per multiply instead of
 // ~825, measured 67.7 G vs 59.8 G fp_mul/s on one MI355X (tools/fpbench.hip, profiles/).
 // Product scanning with interleaved reduction (FIPS): column k adds a_j b_{k-j} + m_j p_{k-j};
-// m_k = (low 28 bits of the column) * (-p^-1) mod 2^28. With inputs < p the result is < 2p (4p < R),
-// so one conditional subtraction in the 32-bit form restores [0, p).
+// m_k = (low 28 bits of the column) * (-p^-1) mod 2^28. The result (< 2p, see above) is returned as
+// it is; fp_canon adds the conditional subtraction where a canonical value is needed.
 // Constants (bls_constants.h) are generated for R = 2^392 (gen_constants.py).
 constexpr uint32_t M28 = (1u << 28) - 1u;
 
@@ -178,21 +205,14 @@ DI void fp_split28(const u12& a, uint32_t (&x)[14]) {
   }
 }
 
-// 14 x 28-bit limbs (top limb < 2^18, value < 2p) -> canonical 12 x 32-bit
-DI u12 fp_join28_reduce(const uint32_t (&t)[14]) {
-  uint32_t r32[12];
+// 14 x 28-bit limbs (top limb < 2^18, value < 2p) -> 12 x 32-bit, still < 2p
+DI u12 fp_join28(const uint32_t (&t)[14]) {
+  u12 r;
 #pragma unroll
   for (int w = 0; w < 12; w++) {
     const int k = (32 * w) / 28, s = (32 * w) % 28;  // s <= 24: two limbs cover the word
-    r32[w] = (t[k] >> s) | (t[k + 1] << (28 - s));
+    r[w] = (t[k] >> s) | (t[k + 1] << (28 - s));
   }
-  uint32_t d[12];
-  unsigned br = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(r32[i], P_RAW[i], br, &br);
-  u12 r;
-#pragma unroll
-  for (int i = 0; i < 12; i++) r[i] = br ? r32[i] : d[i];
   return r;
 }
 
@@ -225,7 +245,7 @@ NOINL u12 fp_mul_u12(u12 a, u12 b) {
     acc >>= 28;
   }
   t[13] = (uint32_t)acc;  // < 2^18: the result is < 2p < 2^382
-  return fp_join28_reduce(t);
+  return fp_join28(t);
 }
 
 // Montgomery square: the cross products x_j x_{k-j} (j < k-j) appear twice, so they are taken once
@@ -256,16 +276,23 @@ NOINL u12 fp_sqr_u12(u12 a) {
     }
   }
   t[13] = (uint32_t)acc;
-  return fp_join28_reduce(t);
+  return fp_join28(t);
 }
 
-// 4p - a for a in [0, 4p] (12-word borrow chain): -a mod p for a lazily-reduced operand
+// 4p - a for a in [0, 4p] (12-word borrow chain)
 DI u12 fp_4p_minus_u12(const u12& a) {
   u12 r;
   unsigned br = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) r[i] = __builtin_subc(P4_RAW[i], a[i], br, &br);
   return r;
+}
+
+// 16p - y limb-wise for a split operand y < 8p (28-bit limbs): every limb of NEG28_16P is at least any
+// such limb, so there are no borrows; the limbs stay below 2^29 (a multiplier operand, never stored)
+DI void fp_neg28(const uint32_t (&y)[14], uint32_t (&r)[14]) {
+#pragma unroll
+  for (int k = 0; k < 14; k++) r[k] = NEG28_16P[k] - y[k];
 }
 
 // a + b as a 12-word integer (no reduction: a, b < 2p keep the sum < 2^384)
@@ -279,10 +306,9 @@ DI u12 fp_add_raw_u12(const u12& a, const u12& b) {
 
 typedef uint32_t u24 __attribute__((ext_vector_type(24)));
 
-// Montgomery "dot product" with one reduction (lazy reduction), operands in radix 2^28:
-//   DOT:  r = (x0 y0 + x1 y1) R^-1        !DOT: r = x0 y0 R^-1
-// Every operand is < 2p; a sum of two products is < 8p^2, so the result is < 8p^2/R + p < 2p and
-// one conditional subtraction makes it canonical. Column sums stay < 2^62.
+// Montgomery "dot product" with one reduction (lazy reduction), operands in radix 2^28 with limbs
+// below 2^29 (operand contract above fp_mul_u12):
+//   DOT:  r = (x0 y0 + x1 y1) R^-1        !DOT: r = x0 y0 R^-1         (r < 2p)
 template <bool DOT>
 DI u12 fp_mont_dot(const uint32_t (&x0)[14], const uint32_t (&y0)[14], const uint32_t (&x1)[14],
                    const uint32_t (&y1)[14]) {
@@ -309,7 +335,7 @@ DI u12 fp_mont_dot(const uint32_t (&x0)[14], const uint32_t (&y0)[14], const uin
     c >>= 28;
   }
   t[13] = (uint32_t)c;
-  return fp_join28_reduce(t);
+  return fp_join28(t);
 }
 
 DI u12 u24_lo(const u24& v) {
@@ -354,22 +380,25 @@ DI void fp2_arg_store(const u24& b) {
 }
 
 // Fp2 product (a0 + a1 i)(b0 + b1 i) in one body:
-//   c0 = a0 b0 + a1 (4p - b1), c1 = a0 b1 + a1 b0
+//   c0 = a0 b0 + a1 (16p - b1), c1 = a0 b1 + a1 b0
 // i.e. two reductions instead of three multiplications' worth (counted as the 3 of Karatsuba).
 DI u24 fp2_mul_body(const u24& a, const u12& b0, const u12& b1) {
-  uint32_t x0[14], x1[14], y0[14], y1[14];
+  uint32_t x0[14], x1[14], y0[14], y1[14], yn[14];
   fp_split28(u24_lo(a), x0);
   fp_split28(u24_hi(a), x1);
   fp_split28(b0, y0);
-  fp_split28(fp_4p_minus_u12(b1), y1);
-  const u12 c0 = fp_mont_dot<true>(x0, y0, x1, y1);
-  BLS_SCHED_FENCE();
   fp_split28(b1, y1);
+  fp_neg28(y1, yn);
+  const u12 c0 = fp_mont_dot<true>(x0, y0, x1, yn);
+  BLS_SCHED_FENCE();
   const u12 c1 = fp_mont_dot<true>(x0, y1, x1, y0);
   return u24_of(c0, c1);
 }
 
-// Fp2 square: c0 = (a0 + a1)(a0 + 4p - a1), c1 = (2 a0) a1
+// Fp2 square: c0 = (a0 + a1)(a0 + 4p - a1), c1 = (2 a0) a1. A squaring operand is at most ONE lazy
+// sum (< 4p; every fp2_sqr* call site squares a reduced value or one fp2_add_lazy), so the 12-word
+// sums stay below 8p < 2^384 (a smaller live set than radix-2^28 sums: the inlined cyclotomic squares
+// of the 3-lane final exponentiation are register-bound).
 DI u24 fp2_sqr_body(const u24& a) {
   const u12 a0 = u24_lo(a), a1 = u24_hi(a);
   uint32_t x[14], y[14];
@@ -431,10 +460,11 @@ DI fp fp_mul8(const fp& a) { return fp_dbl(fp_mul4(a)); }
 
 DI fp fp_to_mont(const fp& raw) { return fp_mul(raw, fp_load_const(FP_R2)); }
 
+// canonical raw value in [0, p)
 DI fp fp_from_mont(const fp& a) {
   fp one = fp_zero();
   one.l[0] = 1;
-  return fp_mul(a, one);
+  return fp_canon(fp_mul(a, one));
 }
 
 // a^e for a public exponent given as little-endian 32-bit words (uniform across the wave ->

@@ -279,7 +279,9 @@ DI g2j iso_map_g2(const g2a& p) {
   return {X, Y, Z};  // Z == 0 (exceptional isogeny kernel) gives the point at infinity
 }
 
-DI g2j hash_field_to_g2(const fp2& u0, const fp2& u1) {
+// the two mapped points q0 = iso(map(u0)), q1 = iso(map(u1)) (Jacobian): the exponentiation-heavy
+// half of hash-to-G2 (one inversion, four Fp exponentiations)
+DI void hash_field_to_q(const fp2& u0, const fp2& u1, g2j& q0, g2j& q1) {
   // one inversion for both SSWU denominators (exact also when one of them is 0: inv0(0) = 0)
   fp2 d0 = sswu_den(u0), d1 = sswu_den(u1);
   const bool z0 = fp2_is_zero(d0), z1 = fp2_is_zero(d1);
@@ -288,8 +290,13 @@ DI g2j hash_field_to_g2(const fp2& u0, const fp2& u1) {
   fp2 di = fp2_inv(fp2_mul(d0, d1));
   fp2 tv0 = fp2_select(z0, fp2_zero(), fp2_mul(d1, di));
   fp2 tv1 = fp2_select(z1, fp2_zero(), fp2_mul(d0, di));
-  g2j q0 = iso_map_g2(map_to_curve_sswu(u0, tv0));
-  g2j q1 = iso_map_g2(map_to_curve_sswu(u1, tv1));
+  q0 = iso_map_g2(map_to_curve_sswu(u0, tv0));
+  q1 = iso_map_g2(map_to_curve_sswu(u1, tv1));
+}
+
+DI g2j hash_field_to_g2(const fp2& u0, const fp2& u1) {
+  g2j q0, q1;
+  hash_field_to_q(u0, u1, q0, q1);
   return g2_clear_cofactor(jac_add(q0, q1));
 }
 

@@ -4,8 +4,15 @@
 
 namespace blsk {
 
+// Two kernels: decoding (flag, infinity form, x < p, the Fp2 square root -- two Fp exponentiations with
+// a small live state, run at high occupancy) and the psi subgroup check ([x] chain on a Jacobian point:
+// many short calls). The reject order is kilic's: the subgroup check only runs on decoded points.
+#ifndef BLS_WPE_SUBGROUP
+#define BLS_WPE_SUBGROUP 1
+#endif
+
 BLS_KERNEL(BLS_WPE_DECOMP) k_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, size_t base,
-                                                       size_t cnt, uint32_t* S, uint8_t* s_inf, uint8_t* cls) {
+                                           size_t cnt, uint32_t* S, uint8_t* s_inf, uint8_t* cls) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt) return;
   uint8_t buf[96];
@@ -13,7 +20,7 @@ BLS_KERNEL(BLS_WPE_DECOMP) k_decompress_g2(const uint8_t* sigs, size_t stride, s
   for (int k = 0; k < 96; k++) buf[k] = p[k];
   g2a a;
   bool inf;
-  uint8_t c = g2_decompress(buf, a, inf, true);
+  uint8_t c = g2_decompress(buf, a, inf, false);
   if (c != REJ_OK) {
     a.x = fp2_zero();
     a.y = fp2_zero();
@@ -23,6 +30,18 @@ BLS_KERNEL(BLS_WPE_DECOMP) k_decompress_g2(const uint8_t* sigs, size_t stride, s
   st_fp2(S, cnt, i, 2, a.y);
   s_inf[i] = inf;
   cls[i] = c;
+}
+
+BLS_KERNEL(BLS_WPE_SUBGROUP) k_subgroup_g2(uint32_t* S, uint8_t* s_inf, uint8_t* cls, size_t cnt) {
+  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= cnt || cls[i] != REJ_OK || s_inf[i]) return;
+  const g2a a = {ld_fp2(S, cnt, i, 0), ld_fp2(S, cnt, i, 2)};
+  if (!g2_in_subgroup(jac_from_aff(a))) {
+    st_fp2(S, cnt, i, 0, fp2_zero());
+    st_fp2(S, cnt, i, 2, fp2_zero());
+    s_inf[i] = 1;
+    cls[i] = REJ_NOT_IN_SUBGROUP;
+  }
 }
 
 // first_bad receives label0 + (index of the first reject): label0 = first_round gives the ROUND
@@ -50,6 +69,7 @@ void launch_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, siz
   if (!cnt) return;
   hipLaunchKernelGGL(k_decompress_g2, dim3(grid_for(cnt)), dim3(TPB), 0, st, sigs, stride, offset, base, cnt, S,
                      s_inf, cls);
+  hipLaunchKernelGGL(k_subgroup_g2, dim3(grid_for(cnt)), dim3(TPB), 0, st, S, s_inf, cls, cnt);
 }
 
 void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap, unsigned long long* first_bad,

@@ -1,4 +1,4 @@
-// Stage 1: drand message derivation + RFC 9380 hash-to-G2, one lane per beacon.
+// Stage 1: drand message derivation + RFC 9380 hash-to-G2, one lane per beacon, in three kernels.
 // chain.Message / MessageV2 (chain/beacon.go:103-114) -> KyberG2.Hash [ext].
 #include "kcommon.h"
 
@@ -15,8 +15,50 @@ DI void store_h(uint32_t* H, uint8_t* h_inf, size_t cnt, size_t i, const g2j& h)
   h_inf[i] = inf;
 }
 
-BLS_KERNEL(BLS_WPE_HASH) k_hash_chained(ChainedSrc src, size_t base, size_t cnt, uint32_t* H,
-                                                      uint8_t* h_inf) {
+// ------------------------------------------------------------------ three phases
+// Hash-to-G2 runs as three kernels with different register needs, the hand-off in SoA staging Q
+// (72 words per item, stride cnt):
+//   A  message, expand_message_xmd, both SSWU maps, 3-isogeny -> q0, q1 (slots 0..11). One inversion
+//      and four Fp exponentiations: long calls with a small live state, run at high occupancy.
+//   B  q0 + q1, h_eff cofactor clearing (two [x] chains) -> slots 6..11 (P = q0 + q1 parked in 0..5).
+//      Many short calls on two Jacobian points: the register-bound phase.
+//   C  affine conversion (one inversion) and the infinity flag -> H.
+DI void store_q(uint32_t* Q, size_t cnt, size_t i, const g2j& q0, const g2j& q1) {
+  st_fp2(Q, cnt, i, 0, q0.x);
+  st_fp2(Q, cnt, i, 2, q0.y);
+  st_fp2(Q, cnt, i, 4, q0.z);
+  st_fp2(Q, cnt, i, 6, q1.x);
+  st_fp2(Q, cnt, i, 8, q1.y);
+  st_fp2(Q, cnt, i, 10, q1.z);
+}
+DI g2j load_jac(const uint32_t* Q, size_t cnt, size_t i, int slot) {
+  return {ld_fp2(Q, cnt, i, slot), ld_fp2(Q, cnt, i, slot + 2), ld_fp2(Q, cnt, i, slot + 4)};
+}
+DI void store_jac(uint32_t* Q, size_t cnt, size_t i, int slot, const g2j& p) {
+  st_fp2(Q, cnt, i, slot, p.x);
+  st_fp2(Q, cnt, i, slot + 2, p.y);
+  st_fp2(Q, cnt, i, slot + 4, p.z);
+}
+
+#ifndef BLS_WPE_HASH_A
+#define BLS_WPE_HASH_A 4
+#endif
+#ifndef BLS_WPE_HASH_B
+#define BLS_WPE_HASH_B 1
+#endif
+#ifndef BLS_WPE_HASH_C
+#define BLS_WPE_HASH_C 4
+#endif
+
+DI void hash_a_from_msg(const uint32_t (&msg)[8], uint32_t* Q, size_t cnt, size_t i) {
+  fp2 u0, u1;
+  hash_to_field_fp2(msg, u0, u1);
+  g2j q0, q1;
+  hash_field_to_q(u0, u1, q0, q1);
+  store_q(Q, cnt, i, q0, q1);
+}
+
+BLS_KERNEL(BLS_WPE_HASH_A) k_hash_chained(ChainedSrc src, size_t base, size_t cnt, uint32_t* Q) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt) return;
   const size_t g = base + i;
@@ -33,48 +75,75 @@ BLS_KERNEL(BLS_WPE_HASH) k_hash_chained(ChainedSrc src, size_t base, size_t cnt,
   }
   uint32_t msg[8];
   drand_message(msg, prev, prev_len, src.first_round + g);
-  store_h(H, h_inf, cnt, i, hash_to_g2(msg));
+  hash_a_from_msg(msg, Q, cnt, i);
 }
 
-BLS_KERNEL(BLS_WPE_HASH) k_hash_unchained(const uint64_t* rounds, uint64_t first_round, size_t base,
-                                                        size_t cnt, uint32_t* H, uint8_t* h_inf) {
+BLS_KERNEL(BLS_WPE_HASH_A) k_hash_unchained(const uint64_t* rounds, uint64_t first_round, size_t base,
+                                            size_t cnt, uint32_t* Q) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt) return;
   const uint64_t round = rounds ? rounds[base + i] : first_round + base + i;
   uint32_t msg[8];
   drand_message_v2(msg, round);
-  store_h(H, h_inf, cnt, i, hash_to_g2(msg));
+  hash_a_from_msg(msg, Q, cnt, i);
 }
 
-BLS_KERNEL(BLS_WPE_HASH) k_hash_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len,
-                                                       size_t cnt, uint32_t* H, uint8_t* h_inf) {
+BLS_KERNEL(BLS_WPE_HASH_A) k_hash_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len,
+                                           size_t cnt, uint32_t* Q) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt) return;
   uint32_t b0[8];
   xmd_b0_bytes(b0, msgs + off[i], len[i], c_dst);
   fp2 u0, u1;
   xmd_tail_to_field(b0, u0, u1);
-  store_h(H, h_inf, cnt, i, hash_field_to_g2(u0, u1));
+  g2j q0, q1;
+  hash_field_to_q(u0, u1, q0, q1);
+  store_q(Q, cnt, i, q0, q1);
+}
+
+BLS_KERNEL(BLS_WPE_HASH_B) k_hash_cofactor(uint32_t* Q, size_t cnt) {
+  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= cnt) return;
+  store_jac(Q, cnt, i, 0, jac_add(load_jac(Q, cnt, i, 0), load_jac(Q, cnt, i, 6)));
+  const g2j r = g2_clear_cofactor_reload([&]() {
+    size_t j = i;
+    asm volatile("" : "+v"(j));  // re-read P at its two uses, never kept live across the [x] chains
+    return load_jac(Q, cnt, j, 0);
+  });
+  store_jac(Q, cnt, i, 6, r);
+}
+
+BLS_KERNEL(BLS_WPE_HASH_C) k_hash_affine(const uint32_t* Q, size_t cnt, uint32_t* H, uint8_t* h_inf) {
+  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= cnt) return;
+  store_h(H, h_inf, cnt, i, load_jac(Q, cnt, i, 6));
 }
 
 // ------------------------------------------------------------------ launchers
+static void launch_hash_bc(uint32_t* Q, size_t cnt, uint32_t* H, uint8_t* h_inf, hipStream_t st) {
+  hipLaunchKernelGGL(k_hash_cofactor, dim3(grid_for(cnt)), dim3(TPB), 0, st, Q, cnt);
+  hipLaunchKernelGGL(k_hash_affine, dim3(grid_for(cnt)), dim3(TPB), 0, st, Q, cnt, H, h_inf);
+}
+
 void launch_hash_chained(const ChainedSrc& src, size_t base, size_t cnt, uint32_t* H, uint8_t* h_inf,
-                         hipStream_t st) {
+                         uint32_t* Q, hipStream_t st) {
   if (!cnt) return;
-  hipLaunchKernelGGL(k_hash_chained, dim3(grid_for(cnt)), dim3(TPB), 0, st, src, base, cnt, H, h_inf);
+  hipLaunchKernelGGL(k_hash_chained, dim3(grid_for(cnt)), dim3(TPB), 0, st, src, base, cnt, Q);
+  launch_hash_bc(Q, cnt, H, h_inf, st);
 }
 
 void launch_hash_unchained(const uint64_t* rounds, uint64_t first_round, size_t base, size_t cnt, uint32_t* H,
-                           uint8_t* h_inf, hipStream_t st) {
+                           uint8_t* h_inf, uint32_t* Q, hipStream_t st) {
   if (!cnt) return;
-  hipLaunchKernelGGL(k_hash_unchained, dim3(grid_for(cnt)), dim3(TPB), 0, st, rounds, first_round, base, cnt, H,
-                     h_inf);
+  hipLaunchKernelGGL(k_hash_unchained, dim3(grid_for(cnt)), dim3(TPB), 0, st, rounds, first_round, base, cnt, Q);
+  launch_hash_bc(Q, cnt, H, h_inf, st);
 }
 
 void launch_hash_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, size_t cnt, uint32_t* H,
-                          uint8_t* h_inf, hipStream_t st) {
+                          uint8_t* h_inf, uint32_t* Q, hipStream_t st) {
   if (!cnt) return;
-  hipLaunchKernelGGL(k_hash_messages, dim3(grid_for(cnt)), dim3(TPB), 0, st, msgs, off, len, cnt, H, h_inf);
+  hipLaunchKernelGGL(k_hash_messages, dim3(grid_for(cnt)), dim3(TPB), 0, st, msgs, off, len, cnt, Q);
+  launch_hash_bc(Q, cnt, H, h_inf, st);
 }
 
 }  // namespace blsk

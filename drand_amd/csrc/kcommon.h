@@ -20,7 +20,7 @@ static inline unsigned grid_for(size_t n) { return (unsigned)((n + TPB - 1) / TP
 #define BLS_WPE_HASH 1
 #endif
 #ifndef BLS_WPE_DECOMP
-#define BLS_WPE_DECOMP 2
+#define BLS_WPE_DECOMP 4
 #endif
 #ifndef BLS_WPE_LINES
 #define BLS_WPE_LINES 2

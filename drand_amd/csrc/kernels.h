@@ -32,14 +32,16 @@ struct ChainedSrc {
   uint64_t seg_phase;  // 0 for the generator and every host-buffer entry point
 };
 
+// Every hash launcher takes Q: HQ_WORDS x cnt words of SoA staging between its three kernels.
+constexpr int HQ_WORDS = 144;
 void launch_hash_chained(const ChainedSrc& src, size_t base, size_t cnt, uint32_t* H, uint8_t* h_inf,
-                         hipStream_t st);
+                         uint32_t* Q, hipStream_t st);
 // chain.VerifyBeaconV2: msg = sha256(BE64(round)); rounds == nullptr -> first_round + base + i
 void launch_hash_unchained(const uint64_t* rounds, uint64_t first_round, size_t base, size_t cnt, uint32_t* H,
-                           uint8_t* h_inf, hipStream_t st);
+                           uint8_t* h_inf, uint32_t* Q, hipStream_t st);
 // arbitrary messages (Scheme.VerifyRecovered / VerifyPartial / Sign): msg i = msgs[off[i] .. off[i]+len[i])
 void launch_hash_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, size_t cnt,
-                          uint32_t* H, uint8_t* h_inf, hipStream_t st);
+                          uint32_t* H, uint8_t* h_inf, uint32_t* Q, hipStream_t st);
 // 96-byte compressed signatures at sigs + (base+i)*stride + offset
 void launch_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, size_t base, size_t cnt, uint32_t* S,
                           uint8_t* s_inf, uint8_t* cls, hipStream_t st);

@@ -27,7 +27,8 @@ DI bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) & fp_is_zero(a.c1); 
 DI bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) & fp_eq(a.c1, b.c1); }
 DI fp2 fp2_select(bool c, const fp2& a, const fp2& b) { return {fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
 DI fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
-// unreduced sum (< 4p for inputs < 2p): only as a multiplier operand (fp.h operand contract)
+// unreduced sum (< 4p for inputs < 2p; < 8p for two levels): only as a multiplier operand (fp.h
+// operand contract)
 DI fp2 fp2_add_lazy(const fp2& a, const fp2& b) { return {fp_add_lazy(a.c0, b.c0), fp_add_lazy(a.c1, b.c1)}; }
 DI fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
 DI fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }

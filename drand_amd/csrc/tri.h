@@ -199,7 +199,7 @@ NOINL void fp2_mul_slot_u24(u24 a, int sel) {
     b0[k] = sel == 0 ? p0 : q0;
     b1[k] = sel == 0 ? p1 : q1;
   }
-  if (sel == 2) {  // y.a + y.b (< 2p each: the sum stays below 4p, fp.h operand contract)
+  if (sel == 2) {  // y.a + y.b (< 4p each: the sum stays below 8p, fp.h operand contract)
     u12 a0, a1;
 #pragma unroll
     for (int k = 0; k < 12; k++) {
