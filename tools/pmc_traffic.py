@@ -11,7 +11,7 @@ import json
 import sys
 from collections import defaultdict
 
-STAGES = (("k_hash", "hash"), ("k_decompress_g2", "decompress"), ("k_miller", "miller"), ("k_fexp", "final_exp"),
+STAGES = (("k_hash", "hash"), ("k_decompress_g2", "decompress"), ("k_subgroup_g2", "decompress"), ("k_miller", "miller"), ("k_fexp", "final_exp"),
           ("k_finish", "finish"))
 
 
