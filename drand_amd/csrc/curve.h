@@ -146,13 +146,41 @@ DI bool jac_eq(const jac<F>& p, const jac<F>& q) {
   return ex & ey;
 }
 
+// G2 doubling (dbl-2009-l, as jac_dbl) with the Fp2 products expanded in place: the [x] chains of
+// the G2 cofactor clearing and subgroup check run their 63 doublings call-free, so the register
+// allocator sees the whole step instead of the AMDGPU call ABI's caller/callee-saved split.
+DI g2j g2_dbl_inl(const g2j& p) {
+  const fp2 A = fp2_sqr_inl(p.x);
+  const fp2 B = fp2_sqr_inl(p.y);
+  const fp2 C = fp2_sqr_inl(B);
+  const fp2 D = fp2_dbl(fp2_sub(fp2_sub(fp2_sqr_inl(fp2_add(p.x, B)), A), C));
+  const fp2 E = fp2_add(fp2_dbl(A), A);
+  const fp2 X3 = fp2_sub(fp2_sqr_inl(E), fp2_dbl(D));
+  const fp2 C8 = fp2_dbl(fp2_dbl(fp2_dbl(C)));
+  const fp2 Y3 = fp2_sub(fp2_mul_inl(E, fp2_sub(D, X3)), C8);
+  const fp2 Z3 = fp2_dbl(fp2_mul_inl(p.y, p.z));
+  return {X3, Y3, Z3};
+}
+
+#ifndef BLS_G2_DBL_INL
+#define BLS_G2_DBL_INL 1
+#endif
+template <typename F>
+DI jac<F> jac_dbl_chain(const jac<F>& p) {
+  if constexpr (BLS_G2_DBL_INL && sizeof(F) == sizeof(fp2)) {
+    return g2_dbl_inl(p);
+  } else {
+    return jac_dbl(p);
+  }
+}
+
 // [|x|] P, |x| = 0xd201000000010000 (bits 63,62,60,57,48,16): 63 dbl + 5 add
 template <typename F>
 DI jac<F> jac_mul_x_abs(const jac<F>& p) {
   jac<F> acc = p;
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
-    acc = jac_dbl(acc);
+    acc = jac_dbl_chain(acc);
     if ((BLS_X_ABS >> i) & 1ull) acc = jac_add(acc, p);
   }
   return acc;
