@@ -59,6 +59,10 @@ struct blsv_ctx {
   std::vector<ProfRec> recs;
   std::vector<hipEvent_t> event_pool;
   hipStream_t stream = nullptr;
+  // decompression runs beside hash-to-G2 (they are independent): a side stream forked from and
+  // joined back into the launch stream with these two events
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   std::string err;
   // group
   bool has_group = false;
@@ -180,14 +184,36 @@ struct PkSel {
   const uint32_t* idx;  // nullptr -> entry 0
 };
 
+// Stage 1 (hash-to-G2, `hash` launches it on st) and stage 2 (decompression) side by side: the
+// decompression goes to the side stream after everything already queued on st (the previous chunk
+// reads S and cls), and st waits for it before the Miller stage. The two stages fill each other's
+// wave-round tails, and a small batch pays max(hash, decompress) instead of the sum.
+template <typename HashFn>
+static int run_head(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t offset, size_t base, size_t cnt,
+                    hipStream_t st, HashFn hash) {
+  HIPCHK(c, hipEventRecord(c->fork_ev, st));
+  HIPCHK(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
+  {
+    StageTimer tm(c, ST_DECOMP, cnt, c->side);
+    blsk::launch_decompress_g2(d_sigs, stride, offset, base, cnt, c->S.as<uint32_t>(), c->s_inf.as<uint8_t>(),
+                               c->cls.as<uint8_t>(), c->side);
+  }
+  HIPCHK(c, hipEventRecord(c->join_ev, c->side));
+  {
+    StageTimer tm(c, ST_HASH, cnt, st);
+    hash();
+  }
+  HIPCHK(c, hipStreamWaitEvent(st, c->join_ev, 0));
+  return BLSV_OK;
+}
+
+// Stages 3..5 (Miller, final exponentiation, finish) after run_head
 static int run_tail(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t offset, size_t base, size_t cnt,
                     const PkSel& pk, uint64_t* d_bitmap, unsigned long long* d_first_bad, uint8_t* d_cls_out,
                     hipStream_t st, uint64_t label0 = 0) {
-  {
-    StageTimer tm(c, ST_DECOMP, cnt, st);
-    blsk::launch_decompress_g2(d_sigs, stride, offset, base, cnt, c->S.as<uint32_t>(), c->s_inf.as<uint8_t>(),
-                               c->cls.as<uint8_t>(), st);
-  }
+  (void)d_sigs;
+  (void)stride;
+  (void)offset;
   {
     StageTimer tm(c, ST_MILLER, cnt, st);
     blsk::launch_miller(pk.tab, pk.inf, pk.idx, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->S.as<uint32_t>(),
@@ -230,10 +256,8 @@ static int verify_driver(blsv_ctx* c, size_t n, const uint8_t* d_sigs, size_t st
   if (rc) return rc;
   for (size_t base = 0; base < n; base += c->cap) {
     const size_t cnt = std::min(c->cap, n - base);
-    {
-      StageTimer tm(c, ST_HASH, cnt, c->stream);
-      hash(base, cnt);
-    }
+    rc = run_head(c, d_sigs, stride, offset, base, cnt, c->stream, [&]() { hash(base, cnt); });
+    if (rc) return rc;
     rc = run_tail(c, d_sigs, stride, offset, base, cnt, pk, c->bitmap.as<uint64_t>(),
                   c->first_bad.as<unsigned long long>(), reject_class ? c->misc.as<uint8_t>() : nullptr, c->stream);
     if (rc) return rc;
@@ -293,9 +317,12 @@ int blsv_create(int device, blsv_ctx** out) {
   c->device = device;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming);
   if (e != hipSuccess) {
     fprintf(stderr, "blsv_create: %s\n", hipGetErrorString(e));
-    delete c;
+    blsv_destroy(c);  // releases whatever was created
     return BLSV_EHIP;
   }
   *out = c;
@@ -305,10 +332,13 @@ int blsv_create(int device, blsv_ctx** out) {
 void blsv_destroy(blsv_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->stream) {
-    (void)hipStreamSynchronize(c->stream);
-    (void)hipStreamDestroy(c->stream);
+  for (hipStream_t s : {c->stream, c->side}) {
+    if (!s) continue;
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
   }
+  if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+  if (c->join_ev) (void)hipEventDestroy(c->join_ev);
   (void)hipDeviceSynchronize();
   for (auto& r : c->recs) {
     (void)hipEventDestroy(r.a);
@@ -542,6 +572,8 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
   HIPCHK(c, c->bitmap.ensure(((k + 63) / 64) * 8 + 8));
   HIPCHK(c, c->first_bad.ensure(8));
   HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
+  rc = run_head(c, c->in_sigs.as<uint8_t>(), partial_len, 2, 0, k, c->stream, []() {});  // hashed above
+  if (rc) return rc;
   rc = run_tail(c, c->in_sigs.as<uint8_t>(), partial_len, 2, 0, k, pk, c->bitmap.as<uint64_t>(),
                 c->first_bad.as<unsigned long long>(), nullptr, c->stream);
   if (rc) return rc;
@@ -775,10 +807,10 @@ int blsv_verify_chained_dev(blsv_ctx* c, uint64_t first_round, uint64_t seg_len,
                        (uint32_t)seed0_len, seg_phase};
   for (size_t base = 0; base < n; base += c->cap) {
     const size_t cnt = std::min(c->cap, n - base);
-    {
-      StageTimer tm(c, ST_HASH, cnt, st);
+    rc = run_head(c, d_sigs96, 96, 0, base, cnt, st, [&]() {
       blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), st);
-    }
+    });
+    if (rc) return rc;
     rc = run_tail(c, d_sigs96, 96, 0, base, cnt, group_pk(c), d_bitmap, (unsigned long long*)d_first_bad,
                   d_reject_class, st, first_round);  // d_first_bad holds a ROUND (include/blsverify.h)
     if (rc) return rc;

@@ -13,18 +13,21 @@ namespace blsk {
 DI int line_slot(int step, int k) { return (step * 2 + k) * 6; }
 
 // Item g = base + i of the chunk (H/S/F/cls stride cnt); its lines at LN index i (stride sub).
+// The two pairs run in separate workgroups (k = blockIdx.x & 1: the pair of the whole wave), so a
+// beacon's two line chains run side by side: half the latency of one lane walking both, twice the
+// waves (a finer tail), and every store still one 256-byte access per wave.
 BLS_KERNEL(BLS_WPE_LINES)
 k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
                const uint8_t* h_inf, const uint32_t* S, const uint8_t* s_inf, const uint8_t* cls, size_t cnt,
                size_t base, size_t m, size_t sub, uint32_t* LN) {
-  const size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  const int k = (int)(blockIdx.x & 1u);
+  const size_t i = (size_t)(blockIdx.x >> 1) * TPB + threadIdx.x;
   if (i >= m) return;
   const size_t g = base + i;
   if (cls[g] != REJ_OK) return;
   const uint32_t kk = pk_idx ? pk_idx[g] : 0u;
   const bool act[2] = {!(pk_inf[kk] | h_inf[g]), !s_inf[g]};
-#pragma unroll 1
-  for (int k = 0; k < 2; k++) {
+  {
     const uint32_t* Qb = k == 0 ? H : S;
     auto load_q = [&]() {
       size_t j = g;
@@ -134,8 +137,8 @@ void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t
   if (!cnt) return;
   for (size_t b = 0; b < cnt; b += sub) {
     const size_t m = cnt - b < sub ? cnt - b : sub;
-    hipLaunchKernelGGL(k_miller_lines, dim3(grid_for(m)), dim3(TPB), 0, st, pk_tab, pk_inf, pk_idx, H, h_inf, S,
-                       s_inf, cls, cnt, b, m, sub, LN);
+    hipLaunchKernelGGL(k_miller_lines, dim3(2 * grid_for(m)), dim3(TPB), 0, st, pk_tab, pk_inf, pk_idx, H, h_inf,
+                       S, s_inf, cls, cnt, b, m, sub, LN);
     // Below one full wave round of the single-lane pass (1 wave/SIMD x 1024 SIMDs x 64 lanes) the GPU is
     // not full and latency decides: the 3-lane pass runs 27.6 k instructions per lane-step against
     // 73.7 k. At full occupancy the single-lane pass has the higher throughput (profiles/r02_*).
