@@ -99,3 +99,11 @@ def test_host_build_decode_classes(opcount_bin, golden):
             prev = mx["genesis_seed"] if i == 0 else mx["sigs"][i - 1]
             rc, out = run_opcount(opcount_bin, mx["pk"], i + 1, prev, mx["sigs"][i])
             assert out.get("class") == c, (i, out)
+
+
+def test_host_build_inversion_matches_exponentiation(opcount_bin):
+    """fp_inv (Pornin binary GCD, fp.h) == a^(p-2) on 20,000 seeded inputs in [0, 2p) and the edge
+    values 0, 1, p, p-1, 2p-1, p+1 -- the same device source compiled for the host."""
+    r = subprocess.run([opcount_bin, "invfuzz", "20000"], capture_output=True, text=True)
+    out = json.loads(r.stdout)
+    assert r.returncode == 0 and out["bad"] == 0, out

@@ -54,8 +54,44 @@ static int cmd_hash(const char* msghex) {
   return 0;
 }
 
+// fp_inv (binary GCD) against a^(p-2) on n seeded inputs in [0, 2p) plus edge values; prints the
+// number of mismatches or out-of-range results as JSON
+static int cmd_invfuzz(unsigned long n) {
+  using namespace bls;
+  unsigned long long s = 0x9e3779b97f4a7c15ull;
+  auto next = [&]() {
+    s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+    return (uint32_t)(s >> 11);
+  };
+  unsigned long bad = 0;
+  for (unsigned long t = 0; t < n; t++) {
+    fp x;
+    for (int i = 0; i < 12; i++) x.l[i] = next();
+    x.l[11] &= 0x1fffffffu;
+    if (t < 6) {
+      for (int i = 0; i < 12; i++) x.l[i] = (t == 2 || t == 3 || t == 5) ? P_RAW[i] : (t == 4 ? P2_RAW[i] : 0u);
+      if (t == 1) x.l[0] = 1;
+      if (t == 3) x.l[0] -= 1;  // p - 1
+      if (t == 4) x.l[0] -= 1;  // 2p - 1
+      if (t == 5) x.l[0] += 1;  // p + 1
+    }
+    uint32_t d[12];
+    unsigned br = 0;
+    for (int i = 0; i < 12; i++) d[i] = __builtin_subc(x.l[i], P2_RAW[i], br, &br);
+    if (!br) for (int i = 0; i < 12; i++) x.l[i] = d[i];  // into [0, 2p)
+    const fp a = fp_from_u12(fp_inv_bingcd(fp_to_u12(x)));
+    const fp b = fp_from_u12(fp_pow_p_minus_2(fp_to_u12(x)));
+    br = 0;
+    for (int i = 0; i < 12; i++) (void)__builtin_subc(a.l[i], P2_RAW[i], br, &br);
+    bad += !fp_eq(a, b) || !br;
+  }
+  printf("{\"inputs\": %lu, \"bad\": %lu}\n", n, bad);
+  return bad != 0;
+}
+
 int main(int argc, char** argv) {
   if (argc == 3 && !strcmp(argv[1], "hash")) return cmd_hash(argv[2]);
+  if (argc == 3 && !strcmp(argv[1], "invfuzz")) return cmd_invfuzz(strtoul(argv[2], nullptr, 10));
   if (argc != 5) {
     fprintf(stderr, "usage: %s pk48hex round prevhex|- sig96hex   (prev '-' = unchained V2)\n       %s hash msghex\n",
             argv[0], argv[0]);
