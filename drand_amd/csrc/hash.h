@@ -279,10 +279,20 @@ DI g2j iso_map_g2(const g2a& p) {
   return {X, Y, Z};  // Z == 0 (exceptional isogeny kernel) gives the point at infinity
 }
 
-// the two mapped points q0 = iso(map(u0)), q1 = iso(map(u1)) (Jacobian): the exponentiation-heavy
-// half of hash-to-G2 (one inversion, four Fp exponentiations)
+// one mapped point q = iso(map(u)) (Jacobian) with its own SSWU denominator inversion (a binary-GCD
+// inversion is cheap, fp.h, so the two points of a hash are independent and can run in two lanes):
+// tv = 1/(Z^2 u^4 + Z u^2), or 0 when that is 0 (RFC 9380 inv0)
+DI g2j hash_field_to_q1(const fp2& u) {
+  const fp2 d = sswu_den(u);
+  const bool z = fp2_is_zero(d);
+  const fp2 tv = fp2_select(z, fp2_zero(), fp2_inv(fp2_select(z, fp2_one(), d)));
+  return iso_map_g2(map_to_curve_sswu(u, tv));
+}
+
+// the two mapped points q0 = iso(map(u0)), q1 = iso(map(u1)) in one lane: the exponentiation-heavy
+// half of hash-to-G2 (one inversion shared by both SSWU denominators, four Fp exponentiations)
 DI void hash_field_to_q(const fp2& u0, const fp2& u1, g2j& q0, g2j& q1) {
-  // one inversion for both SSWU denominators (exact also when one of them is 0: inv0(0) = 0)
+  // exact also when one of the denominators is 0: inv0(0) = 0
   fp2 d0 = sswu_den(u0), d1 = sswu_den(u1);
   const bool z0 = fp2_is_zero(d0), z1 = fp2_is_zero(d1);
   d0 = fp2_select(z0, fp2_one(), d0);

@@ -197,7 +197,9 @@ int blsv_sign(blsv_ctx* ctx, const uint8_t* sk32, int32_t index, const uint8_t* 
  * the ROUND of the first reject or UINT64_MAX), d_reject_class (optional, n bytes). Asynchronous
  * on `stream` (a hipStream_t; NULL = the context stream). The context's staging buffers are shared
  * by every call: successive *_dev calls on one context must be issued on ONE stream (or the caller
- * orders them with events), never concurrently on two streams.
+ * orders them with events), never concurrently on two streams. Internally the decompression stage
+ * runs on the context's side stream, forked from `stream` after the work already queued there and
+ * joined back into it (events) before the pairing stage: ordering with respect to `stream` holds.
  */
 int blsv_verify_chained_dev(blsv_ctx* ctx, uint64_t first_round, uint64_t seg_len, uint64_t seg_phase,
                             const uint8_t* d_seeds96, size_t seed0_len, const uint8_t* d_sigs96, size_t n,
