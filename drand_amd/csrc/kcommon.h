@@ -15,10 +15,9 @@ static inline unsigned grid_for(size_t n) { return (unsigned)((n + TPB - 1) / TP
 
 // Waves per SIMD each stage kernel is compiled for (amdgpu_waves_per_eu caps its VGPR budget at
 // 512 / n). 1 = the full 512 VGPR+AGPR budget; 2 = 256 VGPRs, twice the resident waves, some
-// spilling. Chosen per stage from A/B runs on the MI355X (scripts/gpu_variants.sh).
-#ifndef BLS_WPE_HASH
-#define BLS_WPE_HASH 1
-#endif
+// spilling. Chosen per kernel from same-box A/B runs on the MI355X (scripts/gpu_check.sh,
+// DESIGN.md §4.3); the hash-to-G2 phases have their own knobs in k_hash.hip (BLS_WPE_HASH_A/B/C),
+// the subgroup check in k_decomp.hip, the 3-lane kernels in k_miller.hip / k_fexp.hip.
 #ifndef BLS_WPE_DECOMP
 #define BLS_WPE_DECOMP 4
 #endif
