@@ -44,6 +44,20 @@ def test_hash_to_g2_golden(engine, golden):
         assert got == want, f"hash_to_g2 mismatch for msg {v['msg'][:16]}"
 
 
+def test_hash_to_g2_both_phase_a_forms(engine, golden):
+    """Phase A of hash-to-G2 has two forms (k_hash.hip): one lane per (item, point), each SSWU map with
+    its own inversion, for batches up to 64 Ki items; one lane per item with the inversion shared by
+    both maps above. The same messages must give the same points in both."""
+    msgs = [bytes.fromhex(v["msg"]) for v in golden["hash_to_g2"]]
+    extra = [b"round %d" % i for i in range(65537 - len(msgs))]
+    big, inf_big = engine.test_hash_to_g2(msgs + extra)  # > 64 Ki items: shared-inversion form
+    small, inf_small = engine.test_hash_to_g2(msgs + extra[-64:])  # split form
+    k = len(msgs)
+    assert big[:48 * k] == small[:48 * k]
+    assert big[-48 * 64:] == small[48 * k:]
+    assert not any(inf_big) and not any(inf_small)
+
+
 def test_pairing_golden(engine, golden):
     """Engine reduced pairing = e(P, Q)^3 (hard part uses 3*(p^4-p^2+1)/r)."""
     for v in golden["pairing"]:
