@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/blsverify.h"
@@ -188,9 +189,29 @@ struct PkSel {
 // decompression goes to the side stream after everything already queued on st (the previous chunk
 // reads S and cls), and st waits for it before the Miller stage. The two stages fill each other's
 // wave-round tails, and a small batch pays max(hash, decompress) instead of the sum.
+// BLSV_SERIAL_STAGES=1 in the environment runs the two on the launch stream one after the other
+// (profiling: per-kernel durations without the overlap).
+static bool serial_stages() {
+  static const bool on = [] {
+    const char* e = getenv("BLSV_SERIAL_STAGES");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 template <typename HashFn>
 static int run_head(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t offset, size_t base, size_t cnt,
                     hipStream_t st, HashFn hash) {
+  if (serial_stages()) {
+    {
+      StageTimer tm(c, ST_DECOMP, cnt, st);
+      blsk::launch_decompress_g2(d_sigs, stride, offset, base, cnt, c->S.as<uint32_t>(), c->s_inf.as<uint8_t>(),
+                                 c->cls.as<uint8_t>(), st);
+    }
+    StageTimer tm(c, ST_HASH, cnt, st);
+    hash();
+    return BLSV_OK;
+  }
   HIPCHK(c, hipEventRecord(c->fork_ev, st));
   HIPCHK(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
   {

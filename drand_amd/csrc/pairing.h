@@ -28,22 +28,30 @@ DI fp2 fp2_mul_3b(const fp2& c) {
   return fp2_add(fp2_dbl(x4), x4);
 }
 
+// INL: the Fp2 products expanded in place (call-free step, see g2_dbl_inl in curve.h)
+template <bool INL = false>
 DI void miller_dbl_step(g2proj& t, fp2& l00, fp2& l01, fp2& l11, const fp& xp, const fp& yp) {
-  fp2 A = fp2_half(fp2_mul(t.x, t.y));
-  fp2 B = fp2_sqr(t.y);
-  fp2 C = fp2_sqr(t.z);
+  auto mul = [](const fp2& a, const fp2& b) { return INL ? fp2_mul_inl(a, b) : fp2_mul(a, b); };
+  auto sqr = [](const fp2& a) { return INL ? fp2_sqr_inl(a) : fp2_sqr(a); };
+  fp2 A = fp2_half(mul(t.x, t.y));
+  fp2 B = sqr(t.y);
+  fp2 C = sqr(t.z);
   fp2 E = fp2_mul_3b(C);
   fp2 F = fp2_mul3(E);
   fp2 G = fp2_half(fp2_add(B, F));
-  fp2 H = fp2_sub(fp2_sqr(fp2_add_lazy(t.y, t.z)), fp2_add(B, C));
-  fp2 X2 = fp2_sqr(t.x);
+  fp2 H = fp2_sub(sqr(fp2_add_lazy(t.y, t.z)), fp2_add(B, C));
+  fp2 X2 = sqr(t.x);
   l00 = fp2_sub(E, B);
   l01 = fp2_mul_fp(fp2_mul3(X2), xp);
   l11 = fp2_neg(fp2_mul_fp(H, yp));
-  t.x = fp2_mul(A, fp2_sub(B, F));
-  t.y = fp2_sub(fp2_sqr(G), fp2_mul3(fp2_sqr(E)));
-  t.z = fp2_mul(B, H);
+  t.x = mul(A, fp2_sub(B, F));
+  t.y = fp2_sub(sqr(G), fp2_mul3(sqr(E)));
+  t.z = mul(B, H);
 }
+
+#ifndef BLS_LINES_INL
+#define BLS_LINES_INL 0
+#endif
 
 DI void miller_add_step(g2proj& t, const g2a& q, fp2& l00, fp2& l01, fp2& l11, const fp& xp, const fp& yp) {
   fp2 theta = fp2_sub(t.y, fp2_mul(q.y, t.z));
@@ -144,7 +152,7 @@ DI void miller_lines(const g1a& P, LoadQ load_q, Emit emit) {
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
     line l;
-    miller_dbl_step(T, l.a0, l.a1, l.a4, P.x, P.y);
+    miller_dbl_step<BLS_LINES_INL != 0>(T, l.a0, l.a1, l.a4, P.x, P.y);
     emit(step++, l);
     if ((BLS_X_ABS >> i) & 1ull) {
       miller_add_step(T, load_q(), l.a0, l.a1, l.a4, P.x, P.y);
