@@ -56,6 +56,62 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
   }
 }
 
+#ifndef BLS_MF_LDS
+#define BLS_MF_LDS 1
+#endif
+#if BLS_MF_LDS
+// The line-pair product L (5 Fp2: c0.c0, c0.c1, c0.c2, c1.c1, c1.c2) of the current step parks in LDS
+// (one 120-word column per lane: 30 KB per one-wave workgroup, 4 per CU with g_fp2_arg) and is read
+// back at each use, so f (144 words) and the partial products are all that stay in registers.
+static __shared__ uint32_t g_mf_L[120 * BLS_LANES];
+DI void mf_put(int c, const fp2& v) {
+  const unsigned l = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    g_mf_L[(c * 24 + k) * BLS_LANES + l] = v.c0.l[k];
+    g_mf_L[(c * 24 + 12 + k) * BLS_LANES + l] = v.c1.l[k];
+  }
+}
+DI fp2 mf_get(int c) {
+  unsigned l = threadIdx.x;
+  asm volatile("" : "+v"(l));  // read at the use, never kept live
+  fp2 v;
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    v.c0.l[k] = g_mf_L[(c * 24 + k) * BLS_LANES + l];
+    v.c1.l[k] = g_mf_L[(c * 24 + 12 + k) * BLS_LANES + l];
+  }
+  return v;
+}
+// fp6_mul(a, b) (tower.h, Karatsuba) with b's components read through lb
+template <typename LB>
+DI fp6 fp6_mul_lb(const fp6& a, LB lb) {
+  fp2 t0 = fp2_mul(a.c0, lb(0));
+  fp2 t1 = fp2_mul(a.c1, lb(1));
+  fp2 t2 = fp2_mul(a.c2, lb(2));
+  fp2 c0 = fp2_add(fp2_mul_xi(fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c1, a.c2), fp2_add_lazy(lb(1), lb(2))), t1), t2)), t0);
+  fp2 c1 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(lb(0), lb(1))), t0), t1), fp2_mul_xi(t2));
+  fp2 c2 = fp2_add(fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c2), fp2_add_lazy(lb(0), lb(2))), t0), t2), t1);
+  return {c0, c1, c2};
+}
+// pairing.h fp12_mul_by_line_pair with L read from LDS (mf_get)
+DI fp12 fp12_mul_by_line_pair_lds(const fp12& f) {
+  const fp6 t0 = fp6_mul_lb(f.c0, [](int c) { return mf_get(c); });
+  fp6 t1;
+  {
+    const fp2 b1 = mf_get(3), b2 = mf_get(4);
+    t1 = fp6_mul_by_12(f.c1, b1, b2);
+  }
+  // Ls = (L.c0.c0, L.c0.c1 + L.c1.c1, L.c0.c2 + L.c1.c2)
+  const fp6 c1 = fp6_sub(fp6_sub(fp6_mul_lb(fp6_add_lazy(f.c0, f.c1), [](int c) {
+                                   return c == 0 ? mf_get(0) : fp2_add_lazy(mf_get(c), mf_get(c + 2));
+                                 }),
+                                 t0),
+                         t1);
+  return {fp6_add(t0, fp6_mul_v(t1)), c1};
+}
+#endif
+
 BLS_KERNEL(BLS_WPE_MILLER_F) k_miller_f(const uint32_t* LN, const uint8_t* cls, size_t cnt, size_t base,
                                                   size_t m, size_t sub, uint32_t* F) {
   const size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
@@ -66,7 +122,32 @@ BLS_KERNEL(BLS_WPE_MILLER_F) k_miller_f(const uint32_t* LN, const uint8_t* cls, 
     const int s = line_slot(step, k);
     return line{ld_fp2(LN, sub, i, s + 0), ld_fp2(LN, sub, i, s + 2), ld_fp2(LN, sub, i, s + 4)};
   };
+#if BLS_MF_LDS
+  // miller_f_from_lines (pairing.h) with the line-pair product parked in LDS
+  fp12 f = fp12_one();
+  int step = 0;
+#pragma unroll 1
+  for (int b = 62; b >= 0; b--) {
+#pragma unroll 1
+    for (int rep = 0; rep < 2; rep++) {
+      if (rep == 1 && !((BLS_X_ABS >> b) & 1ull)) break;
+      if (rep == 0 && b != 62) f = fp12_sqr(f);
+      {
+        const fp12 L = line_mul_line(load(step, 0), load(step, 1));
+        mf_put(0, L.c0.c0);
+        mf_put(1, L.c0.c1);
+        mf_put(2, L.c0.c2);
+        mf_put(3, L.c1.c1);
+        mf_put(4, L.c1.c2);
+      }
+      f = fp12_mul_by_line_pair_lds(f);
+      step++;
+    }
+  }
+  st_fp12(F, cnt, g, fp12_conj(f));
+#else
   st_fp12(F, cnt, g, miller_f_from_lines(load));
+#endif
 }
 
 // ------------------------------------------------------------------ 3-lane f pass (tri.h)
