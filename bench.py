@@ -289,6 +289,11 @@ def main():
         "gate": "all rounds accept; negative control (one bit-flipped signature per rank) rejects exactly it and "
                 "the next round, first_bad = lowest corrupted round",
     }
+    if world > 1:  # what the process group actually initialised (the exchange runs over it)
+        out["dist"] = {"backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
+                       "ranks_verified_rounds": sum(counts), "exchange": "all_reduce(MIN first_bad) + "
+                       "all_gather(bitmap words)" + (" + device word-shift repack" if any(c % 64 for c in counts[:-1])
+                                                       else "")}
     if rank == 0 and world == 1 and args.cpu_per_worker > 0 and not strong:  # CPU baseline: rank 0 at N=1 only
         # bounded sample of the same workload: the first whole segments of the rank-0 shard
         workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))

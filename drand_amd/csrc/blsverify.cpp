@@ -70,9 +70,11 @@ struct blsv_ctx {
   size_t t = 0, n = 0;
   DBuf commits, commit_inf;
   std::vector<uint8_t> group_bytes;  // the commitments of the current group (set_group is a no-op on a repeat)
-  // PubPoly.Eval(i) for every share index i < min(n, 65536), computed once per group
+  // PubPoly.Eval(i) for every share index i < min(n, kPkTable), computed once per group on its first
+// partials call; indices beyond the table are evaluated per batch
   DBuf pk_all, pk_all_inf;
   size_t pk_all_n = 0;
+  bool pk_all_built = false;
   // explicit-pk override (verify_messages with pk48)
   DBuf pk_tab, pk_inf;
   uint8_t pk_cache[48];
@@ -391,24 +393,8 @@ int blsv_set_group(blsv_ctx* c, const uint8_t* commits48, size_t t, size_t n) {
   if (rc) return rc;
   for (size_t i = 0; i < t; i++)
     if (cls[i]) return fail(c, BLSV_EINVAL, "set_group: commitment %zu rejected (class %d)", i, (int)cls[i]);
-  // PK_i = PubPoly.Eval(i) for every member index (key/keys.go:239-241; share x = i + 1): the partial
-  // verifications index this table instead of re-running Horner per partial and call
-  const size_t m = std::min<size_t>(n, 65536);
-  c->pk_all_n = 0;
-  if (m) {
-    std::vector<uint32_t> ident(m);
-    for (size_t i = 0; i < m; i++) ident[i] = (uint32_t)i;
-    HIPCHK(c, c->idx.ensure(m * 4));
-    HIPCHK(c, c->pk_all.ensure(m * blsk::G1_WORDS * 4));
-    HIPCHK(c, c->pk_all_inf.ensure(m));
-    HIPCHK(c, hipMemcpyAsync(c->idx.p, ident.data(), m * 4, hipMemcpyHostToDevice, c->stream));
-    blsk::launch_pubpoly_eval(c->commits.as<uint32_t>(), c->commit_inf.as<uint8_t>(), (uint32_t)t,
-                              c->idx.as<uint32_t>(), m, c->pk_all.as<uint32_t>(), c->pk_all_inf.as<uint8_t>(),
-                              c->stream);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipStreamSynchronize(c->stream));  // ident must outlive the copy
-    c->pk_all_n = m;
-  }
+  c->pk_all_n = 0;  // the PK_i table of the new group is built by the first partials call
+  c->pk_all_built = false;
   c->t = t;
   c->n = n;
   c->group_bytes.assign(commits48, commits48 + t * 48);
@@ -537,6 +523,33 @@ int blsv_verify_messages(blsv_ctx* c, const uint8_t* pk48, const uint8_t* msgs, 
 // shared by verify_partials / recover: returns per-partial class in cls (host), S staged on device
 // msg_lens == nullptr: every partial signs the same msg[0 .. msg_len); else partial i signs its own
 // message, msgs packed back to back with msg_lens[i] bytes each.
+constexpr size_t kPkTable = 4096;  // member indices with a precomputed PK_i (drand groups are far smaller)
+
+// PK_i = PubPoly.Eval(i) for every member index below min(n, kPkTable) (key/keys.go:239-241; share
+// x = i + 1), built once per group: the partial verifications index this table instead of running
+// Horner per partial and call. Lazily, on the group's first partials call, so a set_group that is
+// only used for VerifyRecovered never pays the O(t n) G1 work.
+static int ensure_pk_table(blsv_ctx* c) {
+  if (c->pk_all_built) return BLSV_OK;
+  const size_t m = std::min(c->n, kPkTable);
+  if (m) {
+    std::vector<uint32_t> ident(m);
+    for (size_t i = 0; i < m; i++) ident[i] = (uint32_t)i;
+    HIPCHK(c, c->idx.ensure(m * 4));
+    HIPCHK(c, c->pk_all.ensure(m * blsk::G1_WORDS * 4));
+    HIPCHK(c, c->pk_all_inf.ensure(m));
+    HIPCHK(c, hipMemcpyAsync(c->idx.p, ident.data(), m * 4, hipMemcpyHostToDevice, c->stream));
+    blsk::launch_pubpoly_eval(c->commits.as<uint32_t>(), c->commit_inf.as<uint8_t>(), (uint32_t)c->t,
+                              c->idx.as<uint32_t>(), m, c->pk_all.as<uint32_t>(), c->pk_all_inf.as<uint8_t>(),
+                              c->stream);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // ident must outlive the copy
+  }
+  c->pk_all_n = m;
+  c->pk_all_built = true;
+  return BLSV_OK;
+}
+
 static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials,
                           size_t partial_len, size_t k, std::vector<uint8_t>& cls, std::vector<uint32_t>& index,
                           const uint32_t* msg_lens = nullptr) {
@@ -554,7 +567,9 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
     if (partial_len != 98) cls[i] = BLSV_REJ_LENGTH;
   }
   if (partial_len != 98) return BLSV_OK;  // every share has the wrong signature length
-  int rc = ensure_workspace(c, k);
+  int rc = ensure_pk_table(c);
+  if (rc) return rc;
+  rc = ensure_workspace(c, k);
   if (rc) return rc;
   // H(msg) once per item slot (all identical); the per-item PubPoly.Eval(index) table
   std::vector<uint32_t> lens(k, (uint32_t)msg_len);

@@ -600,7 +600,12 @@ DI fp fp_lincomb_mont56(const uint32_t (&X)[14], const uint32_t (&Y)[14], int64_
   return r;
 }
 
-NOINL u12 fp_inv_bingcd(u12 yin) {
+// The GCD proper. *converged = (b == 1 at the end, or y == 0): the exact algorithm needs at most
+// 2*381 - 1 = 761 divsteps and 25 x 31 = 775 run here, but the 64-bit approximations carry no proof
+// of that bound for every input, so the caller checks it (fp_inv_bingcd) and the host fuzz
+// (tools/opcount invfuzz: random, structured 2^k / p - 2^k / (p +- 1) / 2^k / near-p inputs) counts
+// any input that does not converge.
+DI u12 fp_inv_bingcd_raw(u12 yin, bool& converged) {
   uint32_t a[12], b[12];
   const fp yc = fp_canon(fp_from_u12(yin));
 #pragma unroll
@@ -653,7 +658,19 @@ NOINL u12 fp_inv_bingcd(u12 yin) {
     u = fp_lincomb_mont56(X, Y, f0, g0);
     v = fp_lincomb_mont56(X, Y, f1, g1);
   }
+  uint32_t nb = b[0] ^ 1u;
+#pragma unroll
+  for (int i = 1; i < 12; i++) nb |= b[i];
+  converged = (nb == 0) | fp_raw_is_zero(yc);
   return fp_to_u12(fp_mul(v, fp_load_const(FP_INV_FIX)));
+}
+
+NOINL u12 fp_inv_bingcd(u12 yin) {
+  bool ok;
+  u12 r = fp_inv_bingcd_raw(yin, ok);
+  // never taken on any input the fuzz has seen; a lane that did not converge gets the exponentiation
+  if (!ok) r = fp_pow_p_minus_2(yin);
+  return r;
 }
 
 #ifndef BLS_INV_POW

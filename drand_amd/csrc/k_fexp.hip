@@ -25,11 +25,8 @@ BLS_KERNEL(BLS_WPE_FEXP) k_fexp_step(const uint32_t* X, const uint32_t* C, const
     return ld_fp12(B, cnt, j);
   };
   fp12 r = fexp_step<MODE>([&]() { return at(X); }, [&]() { return at(C); }, [&]() { return at(G); });
-  if (MODE < 4) {
-    st_fp12(OUT, cnt, i, r);
-  } else if (!fp12_is_one(r)) {
-    cls[i] = REJ_PAIRING;
-  }
+  if (MODE < 4 || OUT) st_fp12(OUT, cnt, i, r);  // MODE 4 with OUT: the final value (blsv_test_final_exp)
+  if (MODE == 4 && !fp12_is_one(r)) cls[i] = REJ_PAIRING;
 }
 
 // ------------------------------------------------------------------ 3-lane hard part (tri.h)
@@ -109,8 +106,7 @@ void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStr
   hipLaunchKernelGGL(k_fexp_step<1>, grid, blk, 0, st, F, nullptr, nullptr, cnt, cls, B);  // b -> B
   hipLaunchKernelGGL(k_fexp_step<2>, grid, blk, 0, st, B, nullptr, nullptr, cnt, cls, C);  // c -> C
   hipLaunchKernelGGL(k_fexp_step<3>, grid, blk, 0, st, C, nullptr, nullptr, cnt, cls, F);  // t -> F
-  hipLaunchKernelGGL(k_fexp_step<4>, grid, blk, 0, st, F, C, G, cnt, cls, nullptr);
-  (void)out;
+  hipLaunchKernelGGL(k_fexp_step<4>, grid, blk, 0, st, F, C, G, cnt, cls, out);  // out: test hook
   (void)park;
 #else
   const dim3 tgrid((unsigned)((cnt + TRI_GROUPS - 1) / TRI_GROUPS));

@@ -17,7 +17,7 @@ DI void store_h(uint32_t* H, uint8_t* h_inf, size_t cnt, size_t i, const g2j& h)
 
 // ------------------------------------------------------------------ three phases
 // Hash-to-G2 runs as three kernels with different register needs, the hand-off in SoA staging Q
-// (72 words per item, stride cnt):
+// (HQ_WORDS = 144 words per item, stride cnt: two Jacobian G2 points, slots 0..5 and 6..11):
 //   A  message, expand_message_xmd, both SSWU maps, 3-isogeny -> q0, q1 (slots 0..11): inversions and
 //      four Fp exponentiations, long calls with a small live state, run at high occupancy (two forms,
 //      see below).

@@ -155,19 +155,33 @@ def assemble_bitmap(words, counts, stride):
 
 def repack_words(gathered, counts, stride):
     """Device form of assemble_bitmap: per-shard words (shard r at gathered[r*stride:]) -> one
-    bitmap at global bit offsets, with torch ops on the tensor's device (bits unpacked, the shard
-    prefixes concatenated, re-packed; distinct bits make the int64 sum an exact bitwise OR)."""
+    bitmap at global bit offsets. Word-level bit-offset shifts with torch ops on the tensor's device:
+    shard r, starting at global bit pos = 64 q + s, ORs (w << s) into words q.. and the spill
+    (w >>> (64 - s)) into words q+1..; O(words) per shard, no per-bit temporaries (a 100M-round
+    bitmap is 1.56M words)."""
     import torch
 
     dev = gathered.device
-    shifts = torch.arange(64, dtype=torch.int64, device=dev)
-    bits = ((gathered.reshape(len(counts), stride, 1) >> shifts) & 1).reshape(len(counts), stride * 64)
-    flat = torch.cat([bits[r, :c] for r, c in enumerate(counts)])
     total = int(sum(counts))
-    out_words = (total + 63) // 64
-    pad = torch.zeros(out_words * 64, dtype=torch.int64, device=dev)
-    pad[:total] = flat
-    return (pad.reshape(out_words, 64) << shifts).sum(dim=1)
+    out = torch.zeros(max(1, (total + 63) // 64), dtype=torch.int64, device=dev)
+    pos = 0
+    for r, c in enumerate(counts):
+        nw = (c + 63) // 64
+        if nw == 0:
+            continue
+        w = gathered[r * stride: r * stride + nw].clone()
+        nb = c - 64 * (nw - 1)
+        if nb < 64:
+            w[-1] &= (1 << nb) - 1  # bits past the shard's last beacon
+        q, s = divmod(pos, 64)
+        out[q:q + nw] |= w << s if s else w
+        if s:
+            spill = (w >> (64 - s)) & ((1 << s) - 1)  # logical shift of the int64 words
+            hi = min(nw, out.numel() - q - 1)
+            if hi > 0:
+                out[q + 1:q + 1 + hi] |= spill[:hi]
+        pos += c
+    return out[:(total + 63) // 64]
 
 
 def local_seeds(sl: SegmentedSlice, seg_seeds, gen_sigs):

@@ -102,8 +102,10 @@ def test_host_build_decode_classes(opcount_bin, golden):
 
 
 def test_host_build_inversion_matches_exponentiation(opcount_bin):
-    """fp_inv (Pornin binary GCD, fp.h) == a^(p-2) on 20,000 seeded inputs in [0, 2p) and the edge
-    values 0, 1, p, p-1, 2p-1, p+1 -- the same device source compiled for the host."""
+    """fp_inv (Pornin binary GCD, fp.h) == a^(p-2) on 20,000 seeded inputs in [0, 2p), the edge
+    values 0, 1, p, p-1, 2p-1, p+1, and ~2,100 structured inputs (2^k, 2^k - 1, p - 2^k, (p +- 1)/2^k,
+    p +- d, 2p - d) -- the same device source compiled for the host. The GCD is checked WITHOUT the
+    exponentiation fallback of fp_inv_bingcd: every input must also converge (b == 1)."""
     r = subprocess.run([opcount_bin, "invfuzz", "20000"], capture_output=True, text=True)
     out = json.loads(r.stdout)
-    assert r.returncode == 0 and out["bad"] == 0, out
+    assert r.returncode == 0 and out["bad"] == 0 and out["unconverged"] == 0 and out["structured"] > 2000, out

@@ -59,6 +59,27 @@ def test_assemble_bitmap_unaligned():
     assert shard.assemble_bitmap(words, counts, stride) == _bits_to_words(bits)
 
 
+@pytest.mark.parametrize("counts", [[70, 1, 129, 64], [12_500_000 % 4099 + 1, 4099, 63, 65, 1, 0, 200],
+                                    [64, 64, 64], [1], [127, 129, 1000, 3]])
+def test_repack_words_matches_assemble(counts):
+    """The word-shift device repack (bench.py's unaligned configs[3] shards) equals the host
+    assembler bit for bit, garbage past each shard masked, sign bit (bit 63) included."""
+    rng = random.Random(sum(counts))
+    bits = [rng.random() < 0.6 for _ in range(sum(counts))]
+    stride = max(1, max((c + 63) // 64 for c in counts))
+    words, pos = [], 0
+    for c in counts:
+        w = _bits_to_words(bits[pos:pos + c])
+        w += [0xFFFFFFFFFFFFFFFF] * (stride - len(w))
+        if w and c % 64:
+            w[(c - 1) // 64] |= ~((1 << (c % 64)) - 1) & 0xFFFFFFFFFFFFFFFF  # garbage in the last word
+        words += w
+        pos += c
+    got = shard.repack_words(_to_i64(words), counts, stride)
+    assert [x & shard.NONE_U64 for x in got.tolist()] == shard.assemble_bitmap(words, counts, stride) \
+        == _bits_to_words(bits)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

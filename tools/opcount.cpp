@@ -63,8 +63,51 @@ static int cmd_invfuzz(unsigned long n) {
     s ^= s << 13, s ^= s >> 7, s ^= s << 17;
     return (uint32_t)(s >> 11);
   };
-  unsigned long bad = 0;
-  for (unsigned long t = 0; t < n; t++) {
+  // structured inputs (the shapes that stress the 64-bit approximations: long runs of equal top bits,
+  // values just around p and its halvings): 2^k, 2^k - 1, p - 2^k, (p + 1) / 2^k, (p - 1) / 2^k,
+  // p +- d and 2p - d for small d
+  std::vector<fp> st;
+  auto pow2 = [](int k) {
+    fp r = {};
+    if (k < 384) r.l[k / 32] = 1u << (k % 32);
+    return r;
+  };
+  auto sub = [](const fp& a, const fp& b) {
+    fp r;
+    unsigned br = 0;
+    for (int i = 0; i < 12; i++) r.l[i] = __builtin_subc(a.l[i], b.l[i], br, &br);
+    return r;
+  };
+  auto shr = [](fp a, int k) {
+    for (; k > 0; k--) {
+      for (int i = 0; i < 11; i++) a.l[i] = (a.l[i] >> 1) | (a.l[i + 1] << 31);
+      a.l[11] >>= 1;
+    }
+    return a;
+  };
+  fp P, P1, Pm1, one = pow2(0);
+  for (int i = 0; i < 12; i++) P.l[i] = P_RAW[i];
+  Pm1 = sub(P, one);
+  P1 = sub(P, sub(pow2(0), pow2(1)));  // p + 1 (p - (1 - 2) wraps to p + 1)
+  for (int k = 0; k <= 381; k++) {
+    st.push_back(pow2(k));
+    st.push_back(sub(pow2(k), one));
+    if (k < 381) st.push_back(sub(P, pow2(k)));
+    st.push_back(shr(P1, k));
+    st.push_back(shr(Pm1, k));
+  }
+  for (uint32_t d = 1; d < 64; d++) {
+    fp dd = {};
+    dd.l[0] = d;
+    st.push_back(sub(P, dd));
+    fp p2;
+    for (int i = 0; i < 12; i++) p2.l[i] = P2_RAW[i];
+    st.push_back(sub(p2, dd));
+    st.push_back(sub(P, sub(fp{}, dd)));  // p + d
+  }
+  unsigned long bad = 0, unconverged = 0;
+  const unsigned long total = n + st.size();
+  for (unsigned long t = 0; t < total; t++) {
     fp x;
     for (int i = 0; i < 12; i++) x.l[i] = next();
     x.l[11] &= 0x1fffffffu;
@@ -74,19 +117,24 @@ static int cmd_invfuzz(unsigned long n) {
       if (t == 3) x.l[0] -= 1;  // p - 1
       if (t == 4) x.l[0] -= 1;  // 2p - 1
       if (t == 5) x.l[0] += 1;  // p + 1
+    } else if (t >= n) {
+      x = st[t - n];
     }
     uint32_t d[12];
     unsigned br = 0;
     for (int i = 0; i < 12; i++) d[i] = __builtin_subc(x.l[i], P2_RAW[i], br, &br);
     if (!br) for (int i = 0; i < 12; i++) x.l[i] = d[i];  // into [0, 2p)
-    const fp a = fp_from_u12(fp_inv_bingcd(fp_to_u12(x)));
+    bool conv;
+    const fp a = fp_from_u12(fp_inv_bingcd_raw(fp_to_u12(x), conv));  // the GCD alone, no fallback
     const fp b = fp_from_u12(fp_pow_p_minus_2(fp_to_u12(x)));
     br = 0;
     for (int i = 0; i < 12; i++) (void)__builtin_subc(a.l[i], P2_RAW[i], br, &br);
     bad += !fp_eq(a, b) || !br;
+    unconverged += !conv;
   }
-  printf("{\"inputs\": %lu, \"bad\": %lu}\n", n, bad);
-  return bad != 0;
+  printf("{\"inputs\": %lu, \"structured\": %zu, \"bad\": %lu, \"unconverged\": %lu}\n", total, st.size(), bad,
+         unconverged);
+  return bad != 0 || unconverged != 0;
 }
 
 int main(int argc, char** argv) {
