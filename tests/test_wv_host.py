@@ -1,0 +1,101 @@
+"""The latency engine (drand_amd/csrc/w*.h: one item per wave, one 25-bit limb per lane) compiled
+for the host with wv.h's lane emulation (tools/wvtest) and checked on the CPU against Python
+integers, the reference KAT (key/curve_test.go:10-30) and the golden fixtures. The host build also
+checks every arithmetic contract (operand bounds, subtrahends below their constant) as it runs."""
+import json
+import os
+import random
+import subprocess
+
+import pytest
+
+from oracle import bls12381 as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tools", "wvtest")
+P = O.P
+
+
+@pytest.fixture(scope="module")
+def wvtest():
+    subprocess.run(["make", "-C", os.path.join(ROOT, "tools"), "wvtest"], check=True, capture_output=True)
+    return BIN
+
+
+def run(binary, cmd, lines):
+    r = subprocess.run([binary, cmd], input="\n".join(lines) + "\n", capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r.stdout.strip().split("\n")
+
+
+def _m2(a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+
+def test_field_ops_match_integers(wvtest):
+    rng = random.Random(11)
+    cases = [tuple(rng.randrange(P) for _ in range(4)) for _ in range(40)]
+    cases += [(0, 0, 1, 0), (1, 0, 1, 0), (P - 1, P - 1, P - 1, P - 1), (0, 1, 0, 1), (2 ** 380, 3, 7, 2 ** 200)]
+    out = run(wvtest, "field", [" ".join("%x" % v for v in c) for c in cases])
+    half = (P + 1) // 2
+    for c, line in zip(cases, out):
+        a, b = (c[0], c[1]), (c[2], c[3])
+        f = [int(x, 16) for x in line.split()[:22]]
+        got = [tuple(f[i:i + 2]) for i in range(0, 22, 2)]
+        n = (a[0] ** 2 + a[1] ** 2) % P
+        inv = (a[0] * pow(n, P - 2, P) % P, -a[1] * pow(n, P - 2, P) % P) if n else (0, 0)
+        want = [_m2(a, b), _m2(a, a), (a[0] * b[0] % P, a[1] * b[1] % P), ((a[0] + b[0]) % P, (a[1] + b[1]) % P),
+                ((a[0] - b[0]) % P, (a[1] - b[1]) % P), ((a[0] - a[1]) % P, (a[0] + a[1]) % P), (a[0], -a[1] % P),
+                (a[0] * half % P, a[1] * half % P), inv, (n, n),
+                tuple((x + y + z) % P for x, y, z in zip(_m2(a, b), _m2(b, a), _m2(a, a)))]
+        assert got == want, c
+        eq, z = map(int, line.split()[22:])
+        assert eq == (a == b) and z == (a == (0, 0))
+
+
+def test_hash_to_g2_golden(wvtest, golden):
+    cases = golden["hash_to_g2"]
+    out = run(wvtest, "hash", [h["msg"] or "-" for h in cases])
+    for h, line in zip(cases, out):
+        assert line == "0 %x %x %x %x" % tuple(int(v, 16) for v in h["x"] + h["y"]), h["msg"]
+
+
+def test_decompress_matches_oracle(wvtest, golden):
+    m = golden["mixed"]
+    sigs = [golden["kat"]["sig"]] + [b["sig"] for b in golden["chained"]["beacons"][:4]] + m["sigs"]
+    out = run(wvtest, "decompress", sigs)
+    for s, line in zip(sigs, out):
+        try:
+            pt = O.g2_decompress(bytes.fromhex(s))
+            want = "0 1 0 0 0 0" if pt is None else "0 0 %x %x %x %x" % (pt[0][0], pt[0][1], pt[1][0], pt[1][1])
+        except O.DecodeError as e:
+            want = "%d 0 0 0 0 0" % e.cls
+        assert line == want, s
+
+
+def test_verify_kat_and_chain(wvtest, golden):
+    kat = golden["kat"]
+    ch = golden["chained"]
+    seed = bytes.fromhex(ch["genesis_seed"])
+    lines = ["%s %s %s" % (kat["pk"], kat["msg"], kat["sig"])]
+    beacons = ch["beacons"][:3]
+    for i, b in enumerate(beacons):
+        prev = seed if i == 0 else bytes.fromhex(beacons[i - 1]["sig"])
+        lines.append("%s %s %s" % (ch["pk"], O.message(b["round"], prev).hex(), b["sig"]))
+    # negative controls: the KAT signature on another message, a beacon under the wrong round
+    lines.append("%s %s %s" % (kat["pk"], "00" + kat["msg"], kat["sig"]))
+    lines.append("%s %s %s" % (ch["pk"], O.message(beacons[0]["round"] + 1, seed).hex(), beacons[0]["sig"]))
+    assert run(wvtest, "verify", lines) == ["0"] * 4 + ["7", "7"]
+
+
+@pytest.mark.slow
+def test_verify_mixed_golden_classes(wvtest, golden):
+    """Every reject class of the mixed golden batch (configs[4] classes, chained messages)."""
+    m = golden["mixed"]
+    seed = bytes.fromhex(m["genesis_seed"])
+    sigs = [bytes.fromhex(s) for s in m["sigs"]]
+    lines = []
+    for i, s in enumerate(sigs):
+        prev = seed if i == 0 else sigs[i - 1]
+        lines.append("%s %s %s" % (m["pk"], O.message(i + 1, prev).hex(), s.hex()))
+    assert [int(x) for x in run(wvtest, "verify", lines)] == m["expect_class"]

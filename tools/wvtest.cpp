@@ -1,0 +1,167 @@
+// Host build of the latency engine (drand_amd/csrc/w*.h, -DWV_HOST): the same source as the device
+// kernels, with wv.h emulating the 64 lanes, so tests/test_wv_host.py can check every layer against
+// Python integers and the golden vectors on the CPU.
+//
+// usage: wvtest field   < lines "a0 a1 b0 b1" (hex, raw values < p)  -> one line of results each
+//        wvtest verify  < lines "pk48 msg sig96" (hex)                -> reject class per line
+//        wvtest hash    < lines "msg" (hex)                            -> affine H(msg) raw hex
+//        wvtest pair    < lines "px py qx0 qx1 qy0 qy1" (affine raw)  -> Miller loop + final exp (raw)
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../drand_amd/csrc/wverify.h"
+
+namespace wv {
+uint32_t g_host_lds[LDS_WORDS];
+}
+namespace bls {
+unsigned long long g_fp_mul_count = 0;
+}
+
+using namespace wv;
+
+static std::vector<uint32_t> hex_to_limbs(const std::string& h) {  // 16 x 25-bit limbs of a hex integer
+  std::vector<uint32_t> bits;
+  for (int i = (int)h.size() - 1; i >= 0; i--) {
+    const char c = h[i];
+    const int v = c <= '9' ? c - '0' : (c | 32) - 'a' + 10;
+    for (int b = 0; b < 4; b++) bits.push_back((v >> b) & 1);
+  }
+  std::vector<uint32_t> l(16, 0);
+  for (size_t i = 0; i < bits.size() && i < 400; i++) l[i / 25] |= bits[i] << (i % 25);
+  return l;
+}
+static std::string limbs_to_hex(const V& x, int h) {  // strict limbs of half h -> hex
+  std::vector<int> bits;
+  for (int k = 0; k < 16; k++)
+    for (int b = 0; b < 25; b++) bits.push_back((x.v[32 * h + k] >> b) & 1);
+  std::string s;
+  for (int i = 396; i >= 0; i -= 4) {
+    int v = 0;
+    for (int b = 3; b >= 0; b--) v = v * 2 + (i + b < 400 ? bits[i + b] : 0);
+    s += "0123456789abcdef"[v];
+  }
+  size_t nz = s.find_first_not_of('0');
+  return nz == std::string::npos ? "0" : s.substr(nz);
+}
+static F raw_fp2(const std::string& c0, const std::string& c1) {
+  V x = vsplat(0);
+  const auto a = hex_to_limbs(c0), b = hex_to_limbs(c1);
+  for (int k = 0; k < 16; k++) x.v[k] = a[k], x.v[32 + k] = b[k];
+  return mkF(x, 1.0);
+}
+static F to_mont(const F& raw) { return mulp(raw, cst(WC_R2_DUP)); }
+static std::string out_fp2(const F& a) {
+  const V r = raw_canon(a);
+  return limbs_to_hex(r, 0) + " " + limbs_to_hex(r, 1);
+}
+
+static int cmd_field() {
+  char a0[200], a1[200], b0[200], b1[200];
+  while (scanf("%199s %199s %199s %199s", a0, a1, b0, b1) == 4) {
+    wv_init();
+    const F a = to_mont(raw_fp2(a0, a1)), b = to_mont(raw_fp2(b0, b1));
+    printf("%s", out_fp2(mul2(a, b)).c_str());
+    printf(" %s", out_fp2(sqr2(a)).c_str());
+    printf(" %s", out_fp2(mulp(a, b)).c_str());
+    printf(" %s", out_fp2(add(a, b)).c_str());
+    printf(" %s", out_fp2(sub(a, b)).c_str());
+    printf(" %s", out_fp2(mul_xi(a)).c_str());
+    printf(" %s", out_fp2(conj(a)).c_str());
+    printf(" %s", out_fp2(half(a)).c_str());
+    printf(" %s", out_fp2(inv2(a)).c_str());
+    printf(" %s", out_fp2(norm_dup(a)).c_str());
+    printf(" %s", out_fp2(dot(a, b, b, a, a, a)).c_str());
+    printf(" %d %d", (int)eq2(a, b), (int)is_zero2(a));
+    printf("\n");
+  }
+  return 0;
+}
+
+static std::vector<uint8_t> unhex(const std::string& h) {
+  std::vector<uint8_t> b;
+  for (size_t i = 0; i + 1 < h.size(); i += 2) b.push_back((uint8_t)strtoul(h.substr(i, 2).c_str(), nullptr, 16));
+  return b;
+}
+static void msg_b0(const std::vector<uint8_t>& m, uint32_t (&b0)[8]) {
+  if (m.size() == 32) {
+    uint32_t w[8];
+    for (int i = 0; i < 8; i++) w[i] = (uint32_t)m[4 * i] << 24 | (uint32_t)m[4 * i + 1] << 16 | (uint32_t)m[4 * i + 2] << 8 | m[4 * i + 3];
+    xmd_b0_msg32(w, b0);
+  } else {
+    bls::xmd_b0_bytes(b0, m.data(), (uint32_t)m.size(), bls::DST);
+  }
+}
+
+// verify: "pk48 msg sig96" -> reject class (pk that does not decode: -1)
+static int cmd_verify() {
+  char a[300], b[4000], c[300];
+  while (scanf("%299s %3999s %299s", a, b, c) == 3) {
+    wv_init();
+    const auto pk = unhex(a), msg = unhex(strcmp(b, "-") ? b : ""), sig = unhex(c);
+    bls::g1a P;
+    bool pinf = false;
+    if (bls::g1_decompress(pk.data(), P, pinf) != bls::REJ_OK) {
+      printf("-1\n");
+      continue;
+    }
+    uint32_t b0[8];
+    msg_b0(msg, b0);
+    F sx, sy;
+    bool sinf;
+    const int cls = sig.size() == 96 ? verify_item(sig.data(), b0, P.x.l, P.y.l, pinf, sx, sy, sinf) : bls::REJ_LENGTH;
+    printf("%d\n", cls);
+    fflush(stdout);
+  }
+  return 0;
+}
+
+// hash: "msg" -> "inf x0 x1 y0 y1" (affine raw hex)
+static int cmd_hash() {
+  char b[4000];
+  while (scanf("%3999s", b) == 1) {
+    wv_init();
+    const auto msg = unhex(strcmp(b, "-") ? b : "");
+    uint32_t b0[8];
+    msg_b0(msg, b0);
+    F hx, hy;
+    const bool fin = hash_to_g2(b0, hx, hy);
+    if (!fin) {
+      printf("1 0 0 0 0\n");
+      continue;
+    }
+    printf("0 %s %s\n", out_fp2(hx).c_str(), out_fp2(hy).c_str());
+  }
+  return 0;
+}
+
+// decompress: "sig96" -> "class x0 x1 y0 y1"
+static int cmd_decompress() {
+  char c[300];
+  while (scanf("%299s", c) == 1) {
+    wv_init();
+    const auto sig = unhex(c);
+    F x, y;
+    bool inf;
+    const int cls = g2_decompress(sig.data(), x, y, inf);
+    if (cls || inf) {
+      printf("%d %d 0 0 0 0\n", cls, (int)inf);
+      continue;
+    }
+    printf("0 0 %s %s\n", out_fp2(x).c_str(), out_fp2(y).c_str());
+  }
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc >= 2 && !strcmp(argv[1], "field")) return cmd_field();
+  if (argc >= 2 && !strcmp(argv[1], "verify")) return cmd_verify();
+  if (argc >= 2 && !strcmp(argv[1], "hash")) return cmd_hash();
+  if (argc >= 2 && !strcmp(argv[1], "decompress")) return cmd_decompress();
+  fprintf(stderr, "usage: wvtest field|verify|hash|pair\n");
+  return 2;
+}
