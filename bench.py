@@ -49,6 +49,33 @@ def load_json(rel):
         return json.load(f)
 
 
+def host_cores():
+    """Host cores this process may actually use: the CPUs in its affinity mask, capped by the cgroup
+    CPU quota (the GPU box pins a 16-CPU quota on a many-core host: threads beyond it only queue).
+    Returns (cores, facts) with the nproc / affinity / quota / model behind the choice."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    cores = affinity if quota is None else max(1, min(affinity, int(quota + 0.999)))
+    return cores, {"nproc": os.cpu_count(), "affinity": affinity, "cgroup_cpu_quota": quota, "cpu_model": model}
+
+
 def cpu_baseline(pk48, segments, workers):
     """Time the C oracle (oracle/c/bls_oracle.c: the plain-C restatement of kyber/kilic
     verification -- the reference's Go verifier cannot run in this image) over `segments`, a list
@@ -86,7 +113,7 @@ def main():
     ap.add_argument("--slice", default="", help="R/W: verify shard R of a W-way split in this one process")
     ap.add_argument("--seg-len", type=int, default=64, help="rounds per independently seeded chained segment")
     ap.add_argument("--cpu-per-worker", type=int, default=384, help="C-oracle beacons per host thread (0 = skip)")
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-workers", type=int, default=0, help="host threads for the CPU baseline (0 = all usable cores)")
     args = ap.parse_args()
 
     import numpy as np
@@ -296,7 +323,8 @@ def main():
                                                        else "")}
     if rank == 0 and world == 1 and args.cpu_per_worker > 0 and not strong:  # CPU baseline: rank 0 at N=1 only
         # bounded sample of the same workload: the first whole segments of the rank-0 shard
-        workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+        cores, host = host_cores()
+        workers = args.cpu_workers or cores
         n_seg_cpu = min(len(seeds), max(1, (workers * args.cpu_per_worker + seg - 1) // seg))
         m = min(n, n_seg_cpu * seg)
         sh = sigs[:m].cpu().numpy().tobytes()
@@ -311,7 +339,8 @@ def main():
         out["cpu_baseline"] = {"value": round(rate, 1), "unit": "beacons/s", "cores": workers, "kind": "port",
                                "sample": "%d chained beacons (first %d segments of the rank-0 shard) verified by the C "
                                          "oracle (oracle/c/bls_oracle.c, kilic algorithms) on %d host threads"
-                                         % (cnt, n_seg_cpu, workers)}
+                                         % (cnt, n_seg_cpu, workers),
+                               "host": dict(host, usable_cores=cores)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

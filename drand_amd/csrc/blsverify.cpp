@@ -47,16 +47,28 @@ struct DBuf {
 }  // namespace
 
 // Stage timing (blsv_profile_*): HIP events recorded around every stage launch on the launch stream.
-enum Stage { ST_HASH = 0, ST_DECOMP = 1, ST_MILLER = 2, ST_FEXP = 3, ST_FINISH = 4, ST_N = 5 };
+enum Stage { ST_HASH = 0, ST_DECOMP = 1, ST_MILLER = 2, ST_FEXP = 3, ST_FINISH = 4, ST_LAT = 5, ST_N = 6 };
 struct ProfRec {
   int stage;
   size_t items;
   hipEvent_t a, b;
 };
 
+// Cutover between the latency path (one wave per item, k_lat.hip) and the batch pipeline: a batch of at
+// most this many items runs on the latency path. BLSV_LAT_MAX overrides it (0 = batch pipeline only).
+constexpr size_t kLatMaxDefault = 2048;
+static size_t lat_max_env() {
+  static const size_t v = [] {
+    const char* e = getenv("BLSV_LAT_MAX");
+    return e ? (size_t)strtoull(e, nullptr, 10) : kLatMaxDefault;
+  }();
+  return v;
+}
+
 struct blsv_ctx {
   int device = 0;
   bool prof = false;
+  size_t lat_max = lat_max_env();
   std::vector<ProfRec> recs;
   std::vector<hipEvent_t> event_pool;
   hipStream_t stream = nullptr;
@@ -266,10 +278,33 @@ static void bitmap_words_to_bytes(const std::vector<uint64_t>& w, size_t n, uint
   }
 }
 
-// common host-side driver: hash stage chosen by `hash`, signatures already on device
-template <typename HashFn>
+// latency path of a whole batch (n <= lat_max): `lat(cls)` launches the k_lat kernel writing the
+// classes, then the verdicts go through launch_finish as the pipeline's do
+template <typename LatFn>
+static int run_lat(blsv_ctx* c, size_t n, LatFn lat, uint64_t* d_bitmap, unsigned long long* d_first_bad,
+                   uint8_t* d_cls_out, hipStream_t st, uint64_t label0 = 0) {
+  {
+    StageTimer tm(c, ST_LAT, n, st);
+    lat(c->cls.as<uint8_t>());
+  }
+  blsk::launch_finish(c->cls.as<uint8_t>(), 0, n, d_bitmap, d_first_bad, label0, st);
+  if (d_cls_out) HIPCHK(c, hipMemcpyAsync(d_cls_out, c->cls.p, n, hipMemcpyDeviceToDevice, st));
+  HIPCHK(c, hipGetLastError());
+  return BLSV_OK;
+}
+
+static bool use_lat(const blsv_ctx* c, size_t n) { return n > 0 && n <= c->lat_max; }
+
+struct NoLat {
+  void operator()(uint8_t*) const {}
+};
+
+// common host-side driver: hash stage chosen by `hash`, signatures already on device; `lat` (when
+// given) runs the whole batch on the latency path instead when it is small enough
+template <typename HashFn, typename LatFn = NoLat>
 static int verify_driver(blsv_ctx* c, size_t n, const uint8_t* d_sigs, size_t stride, size_t offset, const PkSel& pk,
-                         HashFn hash, uint8_t* ok_bitmap, uint64_t* first_bad_idx, uint8_t* reject_class) {
+                         HashFn hash, uint8_t* ok_bitmap, uint64_t* first_bad_idx, uint8_t* reject_class,
+                         LatFn lat = LatFn(), bool has_lat = false) {
   const size_t words = (n + 63) / 64;
   HIPCHK(c, c->bitmap.ensure(words * 8 + 8));
   HIPCHK(c, c->first_bad.ensure(8));
@@ -277,7 +312,12 @@ static int verify_driver(blsv_ctx* c, size_t n, const uint8_t* d_sigs, size_t st
   if (reject_class) HIPCHK(c, c->misc.ensure(n + 64));
   int rc = ensure_workspace(c, n);
   if (rc) return rc;
-  for (size_t base = 0; base < n; base += c->cap) {
+  if (has_lat && use_lat(c, n)) {
+    rc = run_lat(c, n, lat, c->bitmap.as<uint64_t>(), c->first_bad.as<unsigned long long>(),
+                 reject_class ? c->misc.as<uint8_t>() : nullptr, c->stream);
+    if (rc) return rc;
+  }
+  for (size_t base = 0; base < n && !(has_lat && use_lat(c, n)); base += c->cap) {
     const size_t cnt = std::min(c->cap, n - base);
     rc = run_head(c, d_sigs, stride, offset, base, cnt, c->stream, [&]() { hash(base, cnt); });
     if (rc) return rc;
@@ -419,12 +459,14 @@ int blsv_verify_chained(blsv_ctx* c, uint64_t first_round, const uint8_t* prev0,
   blsk::ChainedSrc src{c->in_sigs.as<uint8_t>(), c->seeds.as<uint8_t>(), first_round, std::max<uint64_t>(n, 1),
                        (uint32_t)prev0_len};
   uint64_t fb = UINT64_MAX;
+  const PkSel pk = group_pk(c);
   int rc = verify_driver(
-      c, n, c->in_sigs.as<uint8_t>(), 96, 0, group_pk(c),
+      c, n, c->in_sigs.as<uint8_t>(), 96, 0, pk,
       [&](size_t base, size_t cnt) {
         blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
       },
-      ok_bitmap, &fb, reject_class);
+      ok_bitmap, &fb, reject_class,
+      [&](uint8_t* cls) { blsk::launch_lat_chained(src, 0, n, pk.tab, pk.inf, cls, c->stream); }, true);
   if (rc) return rc;
   if (first_bad) *first_bad = fb == UINT64_MAX ? UINT64_MAX : first_round + fb;
   return BLSV_OK;
@@ -447,12 +489,14 @@ int blsv_verify_prevs(blsv_ctx* c, uint64_t first_round, const uint8_t* prevs96,
   // segments of length 1: every round hashes its own prev row (seeds[i]); row 0 uses prev0_len bytes
   blsk::ChainedSrc src{c->in_sigs.as<uint8_t>(), c->seeds.as<uint8_t>(), first_round, 1, (uint32_t)prev0_len};
   uint64_t fb = UINT64_MAX;
+  const PkSel pk = group_pk(c);
   int rc = verify_driver(
-      c, n, c->in_sigs.as<uint8_t>(), 96, 0, group_pk(c),
+      c, n, c->in_sigs.as<uint8_t>(), 96, 0, pk,
       [&](size_t base, size_t cnt) {
         blsk::launch_hash_chained(src, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
       },
-      ok_bitmap, &fb, reject_class);
+      ok_bitmap, &fb, reject_class,
+      [&](uint8_t* cls) { blsk::launch_lat_chained(src, 0, n, pk.tab, pk.inf, cls, c->stream); }, true);
   if (rc) return rc;
   if (first_bad) *first_bad = fb == UINT64_MAX ? UINT64_MAX : first_round + fb;
   return BLSV_OK;
@@ -473,13 +517,19 @@ int blsv_verify_unchained(blsv_ctx* c, const uint64_t* rounds, uint64_t first_ro
     d_rounds = c->in_rounds.as<uint64_t>();
   }
   uint64_t fb = UINT64_MAX;
+  const PkSel pk = group_pk(c);
   int rc = verify_driver(
-      c, n, c->in_sigs.as<uint8_t>(), 96, 0, group_pk(c),
+      c, n, c->in_sigs.as<uint8_t>(), 96, 0, pk,
       [&](size_t base, size_t cnt) {
         blsk::launch_hash_unchained(d_rounds, first_round, base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(),
                                     c->HQ.as<uint32_t>(), c->stream);
       },
-      ok_bitmap, &fb, reject_class);
+      ok_bitmap, &fb, reject_class,
+      [&](uint8_t* cls) {
+        blsk::launch_lat_unchained(d_rounds, first_round, c->in_sigs.as<uint8_t>(), 0, n, pk.tab, pk.inf, cls,
+                                   c->stream);
+      },
+      true);
   if (rc) return rc;
   if (first_bad) *first_bad = fb == UINT64_MAX ? UINT64_MAX : (rounds ? rounds[fb] : first_round + fb);
   return BLSV_OK;
@@ -517,7 +567,13 @@ int blsv_verify_messages(blsv_ctx* c, const uint8_t* pk48, const uint8_t* msgs, 
                                    c->in_len.as<uint32_t>() + base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(),
                                    c->HQ.as<uint32_t>(), c->stream);
       },
-      ok_bitmap, first_bad, reject_class);
+      ok_bitmap, first_bad, reject_class,
+      [&](uint8_t* cls) {
+        blsk::launch_lat_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(),
+                                  c->in_sigs.as<uint8_t>(), 96, 0, n, pk.tab, pk.inf, pk.idx, cls, nullptr, nullptr,
+                                  c->stream);
+      },
+      true);
 }
 
 // shared by verify_partials / recover: returns per-partial class in cls (host), S staged on device
@@ -582,8 +638,6 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
     rc = upload_messages(c, packed.data(), lens.data(), k);
   }
   if (rc) return rc;
-  blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), k,
-                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
   HIPCHK(c, c->idx.ensure(k * 4));
   HIPCHK(c, hipMemcpyAsync(c->idx.p, index.data(), k * 4, hipMemcpyHostToDevice, c->stream));
   // PubPoly.Eval(index): the per-group table when every index is a member index (< n), else
@@ -608,11 +662,26 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
   HIPCHK(c, c->bitmap.ensure(((k + 63) / 64) * 8 + 8));
   HIPCHK(c, c->first_bad.ensure(8));
   HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
-  rc = run_head(c, c->in_sigs.as<uint8_t>(), partial_len, 2, 0, k, c->stream, []() {});  // hashed above
-  if (rc) return rc;
-  rc = run_tail(c, c->in_sigs.as<uint8_t>(), partial_len, 2, 0, k, pk, c->bitmap.as<uint64_t>(),
-                c->first_bad.as<unsigned long long>(), nullptr, c->stream);
-  if (rc) return rc;
+  if (use_lat(c, k)) {
+    // one wave per partial; the decoded sigmas land in S (stride k) for recover_from
+    rc = run_lat(
+        c, k,
+        [&](uint8_t* cls_d) {
+          blsk::launch_lat_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(),
+                                    c->in_sigs.as<uint8_t>(), partial_len, 2, k, pk.tab, pk.inf, pk.idx, cls_d,
+                                    c->S.as<uint32_t>(), c->s_inf.as<uint8_t>(), c->stream);
+        },
+        c->bitmap.as<uint64_t>(), c->first_bad.as<unsigned long long>(), nullptr, c->stream);
+    if (rc) return rc;
+  } else {
+    blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), k,
+                               c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
+    rc = run_head(c, c->in_sigs.as<uint8_t>(), partial_len, 2, 0, k, c->stream, []() {});  // hashed above
+    if (rc) return rc;
+    rc = run_tail(c, c->in_sigs.as<uint8_t>(), partial_len, 2, 0, k, pk, c->bitmap.as<uint64_t>(),
+                  c->first_bad.as<unsigned long long>(), nullptr, c->stream);
+    if (rc) return rc;
+  }
   HIPCHK(c, hipMemcpyAsync(cls.data(), c->cls.p, k, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return BLSV_OK;
@@ -841,6 +910,12 @@ int blsv_verify_chained_dev(blsv_ctx* c, uint64_t first_round, uint64_t seg_len,
   if (rc) return rc;
   blsk::ChainedSrc src{d_sigs96, d_seeds96, first_round, seg_len ? seg_len : std::max<uint64_t>(n, 1),
                        (uint32_t)seed0_len, seg_phase};
+  if (use_lat(c, n)) {
+    const PkSel pk = group_pk(c);
+    return run_lat(
+        c, n, [&](uint8_t* cls) { blsk::launch_lat_chained(src, 0, n, pk.tab, pk.inf, cls, st); }, d_bitmap,
+        (unsigned long long*)d_first_bad, d_reject_class, st, first_round);
+  }
   for (size_t base = 0; base < n; base += c->cap) {
     const size_t cnt = std::min(c->cap, n - base);
     rc = run_head(c, d_sigs96, 96, 0, base, cnt, st, [&]() {
@@ -905,6 +980,13 @@ int blsv_profile_read(blsv_ctx* c, double* ms, uint64_t* launches, uint64_t* ite
 }
 
 // ------------------------------------------------------------------ testing hooks
+size_t blsv_test_set_lat_max(blsv_ctx* c, size_t lat_max) {
+  if (!c) return 0;
+  const size_t prev = c->lat_max;
+  c->lat_max = lat_max;
+  return prev;
+}
+
 int blsv_test_fp_mul(blsv_ctx* c, const uint32_t* a, const uint32_t* b, size_t n, uint32_t* out) {
   if (!c || (n && (!a || !b || !out))) return BLSV_EINVAL;
   (void)hipSetDevice(c->device);

@@ -80,6 +80,7 @@ def main():
     add_dup("H256_R2_DUP", (1 << 256) * R * R % P, montgomery=False)
     add_dup("C408_DUP", pow(2, 408, P), montgomery=False)  # 392-form (batch engine) -> 400-form
     add_dup("C392_DUP", pow(2, 392, P), montgomery=False)  # 400-form -> 392-form
+    add_dup("C416_DUP", pow(2, 416, P), montgomery=False)  # fp.h inverse of a 400-form value -> 400-form
     add_dup("P_DUP", P, montgomery=False)
     add_dup("PM1H_DUP", (P - 1) // 2, montgomery=False)
     add_dup("PP1H_DUP", (P + 1) // 2, montgomery=False)  # x > (p-1)/2  <=>  x >= (p+1)/2

@@ -1,0 +1,109 @@
+// Latency path: one wave verifies one item end to end (wverify.h, limbs across lanes). Used for small
+// batches (blsverify.cpp routes batches up to BLSV_LAT_MAX items here), where the batch pipeline's
+// one-lane-per-item stages would leave the chip idle and pay a serial chain of ~16 M VALU
+// instructions per lane. Same inputs and reject classes as the batch stages; the verdicts then go
+// through launch_finish like theirs.
+#include "kcommon.h"
+#include "wverify.h"
+
+namespace blsk {
+
+__constant__ uint8_t c_lat_dst[DST_LEN] = {66, 76, 83, 95, 83, 73, 71, 95, 66, 76, 83, 49, 50, 51, 56, 49, 71, 50, 95, 88,
+                                           77, 68, 58, 83, 72, 65, 45, 50, 53, 54, 95, 83, 83, 87, 85, 95, 82, 79, 95,
+                                           78, 85, 76, 95};
+
+// sigma for recover_from (affine, batch form: 4 Fp slots, Montgomery R = 2^392, SoA of stride s_n)
+DI void store_sigma(uint32_t* S, uint8_t* s_inf, size_t s_n, size_t i, const wv::F& sx, const wv::F& sy, bool inf) {
+  uint32_t wx[2][12], wy[2][12];
+  if (!inf) {
+    wv::fp2_to392_words(sx, wx);
+    wv::fp2_to392_words(sy, wy);
+  }
+  if (threadIdx.x == 0) {
+    for (int c = 0; c < 2; c++)
+      for (int k = 0; k < 12; k++) {
+        S[(size_t)(c * 12 + k) * s_n + i] = inf ? 0u : wx[c][k];
+        S[(size_t)((2 + c) * 12 + k) * s_n + i] = inf ? 0u : wy[c][k];
+      }
+    s_inf[i] = inf;
+  }
+}
+
+// b0: expand_message_xmd's b_0 of item i's message (wave-uniform scalar work)
+template <typename MsgB0>
+DI void lat_verify(MsgB0 msg_b0, size_t i, const uint8_t* sig, const uint32_t* pk_tab, const uint8_t* pk_inf,
+                   const uint32_t* pk_idx, uint8_t* cls, uint32_t* S, uint8_t* s_inf, size_t s_n) {
+  wv::wv_init();
+  uint32_t b0[8];
+  msg_b0(b0);
+  const uint32_t k = pk_idx ? pk_idx[i] : 0u;
+  const uint32_t* pk = pk_tab + (size_t)k * G1_WORDS;
+  wv::F sx, sy;
+  bool sinf = false;
+  const uint8_t c = wv::verify_item(sig, b0, pk, pk + 12, pk_inf[k] != 0, sx, sy, sinf);
+  if (threadIdx.x == 0) cls[i] = c;
+  if (S && (c == REJ_OK || c == REJ_PAIRING)) store_sigma(S, s_inf, s_n, i, sx, sy, sinf);
+}
+
+__global__ void __launch_bounds__(64) k_lat_chained(ChainedSrc src, size_t base, size_t cnt, const uint32_t* pk_tab,
+                                                    const uint8_t* pk_inf, uint8_t* cls) {
+  const size_t i = blockIdx.x;
+  if (i >= cnt) return;
+  const size_t g = base + i;
+  lat_verify(
+      [&](uint32_t(&b0)[8]) {
+        const size_t seg = (g + src.seg_phase) / src.seg_len;
+        const bool seg_start = g == 0 || (g + src.seg_phase - seg * src.seg_len) == 0;
+        const uint8_t* prev = seg_start ? src.seeds + seg * 96 : src.sigs + (g - 1) * 96;
+        const int prev_len = seg_start ? (seg == 0 ? (int)src.seed0_len : 96) : 96;
+        uint32_t msg[8];
+        drand_message(msg, prev, prev_len, src.first_round + g);
+        wv::xmd_b0_msg32(msg, b0);
+      },
+      i, src.sigs + g * 96, pk_tab, pk_inf, nullptr, cls, nullptr, nullptr, 0);
+}
+
+__global__ void __launch_bounds__(64) k_lat_unchained(const uint64_t* rounds, uint64_t first_round, const uint8_t* sigs,
+                                                      size_t base, size_t cnt, const uint32_t* pk_tab,
+                                                      const uint8_t* pk_inf, uint8_t* cls) {
+  const size_t i = blockIdx.x;
+  if (i >= cnt) return;
+  lat_verify(
+      [&](uint32_t(&b0)[8]) {
+        uint32_t msg[8];
+        drand_message_v2(msg, rounds ? rounds[base + i] : first_round + base + i);
+        wv::xmd_b0_msg32(msg, b0);
+      },
+      i, sigs + (base + i) * 96, pk_tab, pk_inf, nullptr, cls, nullptr, nullptr, 0);
+}
+
+__global__ void __launch_bounds__(64) k_lat_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len,
+                                                     const uint8_t* sigs, size_t stride, size_t offset, size_t cnt,
+                                                     const uint32_t* pk_tab, const uint8_t* pk_inf,
+                                                     const uint32_t* pk_idx, uint8_t* cls, uint32_t* S,
+                                                     uint8_t* s_inf) {
+  const size_t i = blockIdx.x;
+  if (i >= cnt) return;
+  lat_verify([&](uint32_t(&b0)[8]) { xmd_b0_bytes(b0, msgs + off[i], len[i], c_lat_dst); }, i,
+             sigs + i * stride + offset, pk_tab, pk_inf, pk_idx, cls, S, s_inf, cnt);
+}
+
+void launch_lat_chained(const ChainedSrc& src, size_t base, size_t cnt, const uint32_t* pk_tab, const uint8_t* pk_inf,
+                        uint8_t* cls, hipStream_t st) {
+  if (cnt) hipLaunchKernelGGL(k_lat_chained, dim3((unsigned)cnt), dim3(64), 0, st, src, base, cnt, pk_tab, pk_inf, cls);
+}
+void launch_lat_unchained(const uint64_t* rounds, uint64_t first_round, const uint8_t* sigs, size_t base, size_t cnt,
+                          const uint32_t* pk_tab, const uint8_t* pk_inf, uint8_t* cls, hipStream_t st) {
+  if (cnt)
+    hipLaunchKernelGGL(k_lat_unchained, dim3((unsigned)cnt), dim3(64), 0, st, rounds, first_round, sigs, base, cnt,
+                       pk_tab, pk_inf, cls);
+}
+void launch_lat_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, const uint8_t* sigs,
+                         size_t stride, size_t offset, size_t cnt, const uint32_t* pk_tab, const uint8_t* pk_inf,
+                         const uint32_t* pk_idx, uint8_t* cls, uint32_t* S, uint8_t* s_inf, hipStream_t st) {
+  if (cnt)
+    hipLaunchKernelGGL(k_lat_messages, dim3((unsigned)cnt), dim3(64), 0, st, msgs, off, len, sigs, stride, offset, cnt,
+                       pk_tab, pk_inf, pk_idx, cls, S, s_inf);
+}
+
+}  // namespace blsk

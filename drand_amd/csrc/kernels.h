@@ -63,6 +63,16 @@ void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStr
 void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap, unsigned long long* first_bad,
                    uint64_t label0, hipStream_t st);
 
+// ---- latency path (k_lat.hip): one wave per item, the whole verification; writes cls[i] (REJ_*)
+// and, for the messages form with S != nullptr, the decoded sigma (H/S staging layout, stride cnt)
+void launch_lat_chained(const ChainedSrc& src, size_t base, size_t cnt, const uint32_t* pk_tab, const uint8_t* pk_inf,
+                        uint8_t* cls, hipStream_t st);
+void launch_lat_unchained(const uint64_t* rounds, uint64_t first_round, const uint8_t* sigs, size_t base, size_t cnt,
+                          const uint32_t* pk_tab, const uint8_t* pk_inf, uint8_t* cls, hipStream_t st);
+void launch_lat_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, const uint8_t* sigs,
+                         size_t stride, size_t offset, size_t cnt, const uint32_t* pk_tab, const uint8_t* pk_inf,
+                         const uint32_t* pk_idx, uint8_t* cls, uint32_t* S, uint8_t* s_inf, hipStream_t st);
+
 // ---- group / threshold / signing kernels (k_misc.hip)
 // decompress cnt G1 points (48 B each) -> pk table entries + inf flags + reject class
 void launch_decompress_g1(const uint8_t* in, size_t cnt, uint32_t* tab, uint8_t* inf, uint8_t* cls, hipStream_t st);

@@ -26,6 +26,12 @@
 #include "wv.h"
 #include "wv_constants.h"
 #include "bls_constants.h"
+#ifdef WV_HOST
+#ifndef BLS_HOST
+#define BLS_HOST
+#endif
+#endif
+#include "fp.h"  // the batch engine's binary-GCD inversion, run here on wave-uniform values
 
 #ifdef WV_HOST
 #include <execinfo.h>
@@ -482,10 +488,64 @@ WVI F pow_pair(const F& a, const uint32_t (&e)[NW]) {
   }
   return r;
 }
-WVI F inv_pair(const F& a) { return pow_pair<12>(a, bls::EXP_P_MINUS_2); }        // 0 -> 0
+// ------------------------------------------------------------------ inversion by binary GCD
+// Both halves' canonical values are read out (v_readlane) as 12-word integers; fp.h's binary GCD
+// (Pornin, 25 x 31 divsteps on 64-bit approximations) runs on them as wave-uniform scalar code, its
+// exponentiation fallback included; the result goes back into the lanes. The GCD inverts the raw
+// integer a' = A 2^400 as if it were a 2^392-Montgomery value: it returns 2^784 / a', and one
+// product with the constant 2^416 turns that into 2^800 / a' = A^-1 2^400.
+WVI void limbs_to_words(V strict_limbs, int h, uint32_t (&w)[12]) {
+  uint32_t limb[16];
+  for (int k = 0; k < 16; k++) limb[k] = lane_val(strict_limbs, 32 * h + k);
+  for (int j = 0; j < 12; j++) {
+    const int b = 32 * j, k = b / 25, s = b % 25;
+    uint64_t v = (uint64_t)limb[k] >> s;
+    if (k + 1 < 16) v |= (uint64_t)limb[k + 1] << (25 - s);
+    if (k + 2 < 16) v |= (uint64_t)limb[k + 2] << (50 - s);
+    w[j] = (uint32_t)v;
+  }
+}
+// 12-word integers (< 2^384) of half 0 and half 1 -> value-form limbs (not reduced mod p)
+WVI V words_to_limbs(const uint32_t (&w0)[12], const uint32_t (&w1)[12]) {
+  const V l = lane_id(), k = l & 15u;
+  V v = vsplat(0);
+  for (int kk = 0; kk < 16; kk++) {
+    const int bit = 25 * kk, wi = bit >> 5, sh = bit & 31;
+    auto pick = [&](const uint32_t (&w)[12]) {
+      const uint32_t lo = w[wi], hi = wi + 1 < 12 ? w[wi + 1] : 0u;
+      return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & M25;
+    };
+    v = sel(k == (uint32_t)kk, sel(l < 32u, vsplat(pick(w0)), vsplat(pick(w1))), v);
+  }
+  return sel((l & 16u) == 0u, v, vsplat(0));
+}
+WVI void gcd_inverse_words(uint32_t (&w)[12]) {
+  bls::u12 y;
+  for (int i = 0; i < 12; i++) y[i] = w[i];
+  bool conv;
+  bls::u12 r = bls::fp_inv_bingcd_raw(y, conv);
+  if (!conv) r = bls::fp_pow_p_minus_2(y);  // never taken on any input the fuzz has seen (fp.h)
+  for (int i = 0; i < 12; i++) w[i] = r[i];
+}
+// per half: a_h^-1 (0 -> 0); `both` = false when only half 0 is needed (a duplicated value)
+WVI F inv_pair(const F& a, bool both = true) {
+  const V c = canon_times(a, WC_ONE_DUP);
+  uint32_t w0[12], w1[12];
+  limbs_to_words(c, 0, w0);
+  gcd_inverse_words(w0);
+  if (both) {
+    limbs_to_words(c, 1, w1);
+    gcd_inverse_words(w1);
+  } else {
+    for (int i = 0; i < 12; i++) w1[i] = w0[i];
+  }
+  // the GCD's output is < 2p: as a product operand it is a value below 2p
+  return mulp(mkF(words_to_limbs(w0, w1), 2.0), cst(WC_C416_DUP));
+}
+WVI F inv_pair_pow(const F& a) { return pow_pair<12>(a, bls::EXP_P_MINUS_2); }  // 0 -> 0
 WVI F pow_pm3d4(const F& a) { return pow_pair<12>(a, bls::EXP_P_MINUS_3_DIV_4); }  // sqrt and its inverse
-WVI F inv2(const F& a) {  // Fp2: conj(a) / N(a)
-  const F ni = inv_pair(norm_dup(a));
+WVI F inv2(const F& a) {  // Fp2: conj(a) / N(a) (the norm is duplicated: one GCD)
+  const F ni = inv_pair(norm_dup(a), false);
   return mulp(conj<0>(a), ni);
 }
 

@@ -288,7 +288,7 @@ class Engine:
                                                        seed0_len, d_sigs, n, stream))
 
     # ------------------------------------------------------------------ stage profiling
-    STAGES = ("hash", "decompress", "miller", "final_exp", "finish")
+    STAGES = ("hash", "decompress", "miller", "final_exp", "finish", "lat")
 
     def profile(self, on=True):
         self._check(self.lib.blsv_profile_enable(self._h, 1 if on else 0))
@@ -305,6 +305,10 @@ class Engine:
         return {s: (ms[k], la[k], it[k]) for k, s in enumerate(self.STAGES)}
 
     # ------------------------------------------------------------------ testing hooks
+    def set_lat_max(self, n):
+        """Batches of at most n items take the latency path (one wave per item); returns the old cutover."""
+        return self.lib.blsv_test_set_lat_max(self._h, int(n))
+
     def test_fp_mul(self, a_limbs, b_limbs):
         n = len(a_limbs) // 12
         A = (ctypes.c_uint32 * max(len(a_limbs), 1))(*a_limbs)

@@ -27,6 +27,7 @@
  */
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <x86intrin.h>
 
@@ -888,4 +889,189 @@ int bo_g2_decode_class(const uint8_t* sig, size_t len) {
   bo_init();
   g2a s;
   return g2_decompress(sig, len, &s);
+}
+
+/* ================================================================ tbls (threshold) */
+/* Scalars mod r as 4 little-endian 64-bit words (< r). Only the Lagrange coefficients use them, a few
+   thousand products per Recover, so a shift-and-add product is plenty. */
+typedef struct {
+  uint64_t w[4];
+} sc;
+static int sc_geq_r(const uint64_t* a) {
+  for (int i = 3; i >= 0; i--)
+    if (a[i] != C_R_ORDER[i]) return a[i] > C_R_ORDER[i];
+  return 1;
+}
+static sc sc_add(sc a, sc b) { /* a, b < r < 2^255: the sum fits 256 bits */
+  sc s;
+  unsigned __int128 c = 0;
+  for (int i = 0; i < 4; i++) {
+    c += (unsigned __int128)a.w[i] + b.w[i];
+    s.w[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  if (sc_geq_r(s.w)) {
+    __int128 d = 0;
+    for (int i = 0; i < 4; i++) {
+      d += (__int128)s.w[i] - C_R_ORDER[i];
+      s.w[i] = (uint64_t)d;
+      d >>= 64;
+    }
+  }
+  return s;
+}
+static sc sc_neg(sc a) {
+  sc z = {{0, 0, 0, 0}};
+  if (!(a.w[0] | a.w[1] | a.w[2] | a.w[3])) return z;
+  __int128 d = 0;
+  for (int i = 0; i < 4; i++) {
+    d += (__int128)C_R_ORDER[i] - a.w[i];
+    z.w[i] = (uint64_t)d;
+    d >>= 64;
+  }
+  return z;
+}
+static sc sc_mul(sc a, sc b) {
+  sc acc = {{0, 0, 0, 0}};
+  for (int i = 255; i >= 0; i--) {
+    acc = sc_add(acc, acc);
+    if ((b.w[i >> 6] >> (i & 63)) & 1) acc = sc_add(acc, a);
+  }
+  return acc;
+}
+static sc sc_small(uint64_t v) { /* v < r */
+  sc s = {{v, 0, 0, 0}};
+  return s;
+}
+static sc sc_inv(sc a) { /* a^(r-2) */
+  uint64_t e[4];
+  memcpy(e, C_R_ORDER, sizeof e);
+  e[0] -= 2; /* r is odd and its low word is 1 -> no borrow */
+  sc acc = sc_small(1);
+  for (int i = 255; i >= 0; i--) {
+    acc = sc_mul(acc, acc);
+    if ((e[i >> 6] >> (i & 63)) & 1) acc = sc_mul(acc, a);
+  }
+  return acc;
+}
+
+/* [k] P for a small k (share indices): double-and-add from k's top bit */
+static g1j g1_mul_small(g1j p, uint64_t k) {
+  g1j acc = p;
+  acc.z = fp_zero();
+  int top = 63;
+  while (top >= 0 && !((k >> top) & 1)) top--;
+  for (int b = top; b >= 0; b--) {
+    acc = g1_dbl(acc);
+    if ((k >> b) & 1) acc = g1_add(acc, p);
+  }
+  return acc;
+}
+static g1a g1_to_aff(g1j p) {
+  g1a r;
+  r.inf = fp_is_zero(p.z);
+  if (r.inf) return r;
+  fp zi = fp_inv(p.z), zi2 = fp_sqr(zi);
+  r.x = fp_mul(p.x, zi2);
+  r.y = fp_mul(p.y, fp_mul(zi2, zi));
+  return r;
+}
+
+/* the group's public polynomial (share.PubPoly): t decoded commitments */
+typedef struct {
+  int t;
+  g1j c[];
+} bo_group;
+
+void* bo_group_new(const uint8_t* commits48, int t) {
+  bo_init();
+  if (t <= 0) return NULL;
+  bo_group* g = (bo_group*)malloc(sizeof(bo_group) + (size_t)t * sizeof(g1j));
+  if (!g) return NULL;
+  g->t = t;
+  for (int j = 0; j < t; j++) {
+    g1a a;
+    if (g1_decompress(commits48 + 48 * (size_t)j, &a) != REJ_OK) {
+      free(g);
+      return NULL;
+    }
+    g->c[j].x = a.x;
+    g->c[j].y = a.y;
+    g->c[j].z = a.inf ? fp_zero() : FP_ONE;
+  }
+  return g;
+}
+void bo_group_free(void* g) { free(g); }
+
+/* share.PubPoly.Eval(i) = sum_j C_j (i+1)^j by Horner (oracle/bls12381.py pubpoly_eval) */
+static g1a pubpoly_eval(const bo_group* g, unsigned i) {
+  g1j v = g->c[g->t - 1];
+  for (int j = g->t - 2; j >= 0; j--) v = g1_add(g1_mul_small(v, (uint64_t)i + 1), g->c[j]);
+  return g1_to_aff(v);
+}
+
+/* tbls.VerifyPartial (kyber sign/tbls): index = the 2-byte big-endian prefix, then bls.Verify of
+   the rest against PubPoly.Eval(index). Reject class (a share shorter than 2 bytes: REJ_LENGTH). */
+int bo_tbls_verify_partial(const void* gp, const uint8_t* msg, size_t len, const uint8_t* part, size_t plen) {
+  const bo_group* g = (const bo_group*)gp;
+  if (plen < 2) return REJ_LENGTH;
+  const unsigned idx = ((unsigned)part[0] << 8) | part[1];
+  g1a pk = pubpoly_eval(g, idx);
+  return verify_decoded(&pk, msg, len, part + 2, plen - 2);
+}
+
+/* tbls.Recover -> share.RecoverCommit, the same rules as oracle/bls12381.py tbls_recover: walk the
+   shares in input order, skip invalid ones, take valid ones until t are held (a duplicate index
+   counts toward t); keep the last point per index and drop indices >= n; fewer than t distinct ->
+   -1. Otherwise out96 = compress(sum_i lambda_i S_i), lambda_i the Lagrange coefficient at 0 over
+   x = index + 1. parts = `count` shares laid end to end, lens[k] bytes each. */
+int bo_tbls_recover(const void* gp, const uint8_t* msg, size_t len, const uint8_t* parts, const size_t* lens,
+                    size_t count, int t, int n, uint8_t out96[96]) {
+  const bo_group* g = (const bo_group*)gp;
+  if (t <= 0 || n <= 0 || n > 65536) return -1;
+  int* idx = (int*)malloc(sizeof(int) * (size_t)t);
+  g2a* pts = (g2a*)malloc(sizeof(g2a) * (size_t)t);
+  int* slot = (int*)malloc(sizeof(int) * (size_t)n); /* index -> position in the distinct list */
+  if (!idx || !pts || !slot) {
+    free(idx), free(pts), free(slot);
+    return -1;
+  }
+  for (int i = 0; i < n; i++) slot[i] = -1;
+  int taken = 0, distinct = 0;
+  size_t off = 0;
+  for (size_t k = 0; k < count && taken < t; off += lens[k], k++) {
+    const uint8_t* p = parts + off;
+    if (lens[k] < 2 || bo_tbls_verify_partial(g, msg, len, p, lens[k]) != REJ_OK) continue;
+    taken++;
+    const int i = ((int)p[0] << 8) | p[1];
+    if (i >= n) continue;
+    g2a s;
+    g2_decompress(p + 2, lens[k] - 2, &s);
+    if (slot[i] < 0) {
+      slot[i] = distinct;
+      idx[distinct++] = i;
+    }
+    pts[slot[i]] = s;
+  }
+  int rc = -1;
+  if (distinct >= t) {
+    g2j acc = g2_from_aff(pts[0]);
+    acc.z = fp2_zero();
+    for (int a = 0; a < distinct; a++) {
+      sc num = sc_small(1), den = sc_small(1);
+      const sc xa = sc_small((uint64_t)idx[a] + 1);
+      for (int b = 0; b < distinct; b++) {
+        if (b == a) continue;
+        const sc xb = sc_small((uint64_t)idx[b] + 1);
+        num = sc_mul(num, xb);
+        den = sc_mul(den, sc_add(xb, sc_neg(xa)));
+      }
+      const sc lam = sc_mul(num, sc_inv(den));
+      acc = g2_add(acc, g2_mul_words(g2_from_aff(pts[a]), lam.w, 4));
+    }
+    g2_compress(out96, acc);
+    rc = 0;
+  }
+  free(idx), free(pts), free(slot);
+  return rc;
 }

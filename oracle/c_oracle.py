@@ -28,6 +28,12 @@ def load():
         lib.bo_hash_to_g2.argtypes = [c_u8p, ctypes.c_size_t, ctypes.c_char_p]
         lib.bo_sign.argtypes = [c_u8p, c_u8p, ctypes.c_size_t, ctypes.c_char_p]
         lib.bo_g2_decode_class.argtypes = [c_u8p, ctypes.c_size_t]
+        lib.bo_group_new.argtypes = [c_u8p, ctypes.c_int]
+        lib.bo_group_new.restype = ctypes.c_void_p
+        lib.bo_group_free.argtypes = [ctypes.c_void_p]
+        lib.bo_tbls_verify_partial.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_size_t, c_u8p, ctypes.c_size_t]
+        lib.bo_tbls_recover.argtypes = [ctypes.c_void_p, c_u8p, ctypes.c_size_t, c_u8p, ctypes.c_void_p,
+                                        ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
         lib.bo_init()  # constants; must precede any multi-threaded use
         _lib = lib
     return _lib
@@ -62,3 +68,31 @@ def sign(sk: int, msg: bytes) -> bytes:
 
 def g2_decode_class(sig: bytes) -> int:
     return load().bo_g2_decode_class(sig, len(sig))
+
+
+class Group:
+    """share.PubPoly of t G1 commitments (decoded once), for tbls VerifyPartial / Recover."""
+
+    def __init__(self, commits48):
+        self._h = load().bo_group_new(b"".join(commits48), len(commits48))
+        if not self._h:
+            raise ValueError("a commitment does not decode")
+
+    def close(self):
+        if self._h:
+            load().bo_group_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def verify_partial(self, msg: bytes, partial: bytes) -> int:
+        """tbls.VerifyPartial -> reject class (0 = accept)."""
+        return load().bo_tbls_verify_partial(self._h, msg, len(msg), partial, len(partial))
+
+    def recover(self, msg: bytes, partials, t: int, n: int):
+        """tbls.Recover -> 96-byte group signature, or None (not enough good shares)."""
+        lens = (ctypes.c_size_t * max(len(partials), 1))(*[len(p) for p in partials])
+        out = ctypes.create_string_buffer(96)
+        rc = load().bo_tbls_recover(self._h, msg, len(msg), b"".join(partials), ctypes.cast(lens, ctypes.c_void_p),
+                                    len(partials), t, n, out)
+        return out.raw if rc == 0 else None

@@ -66,3 +66,28 @@ def test_cross_check_python_oracle(C):
     sig = C.sign(sk, msg)
     assert sig == O.sign(sk, msg)
     assert C.verify(pk48, msg, sig) == O.verify_class(O.g1_decompress(pk48), msg, sig) == O.REJ_OK
+
+
+def test_threshold_golden(C, golden):
+    """tbls VerifyPartial / Recover of the C oracle (the configs[2] CPU baseline) against the golden
+    n = 64 / t = 33 round made by the Python oracle: every V1 and V2 partial accepts, the bad partial
+    rejects, and Recover reproduces both group signatures byte for byte."""
+    th = golden["threshold"]
+    g = C.Group([bytes.fromhex(c) for c in th["commits"]])
+    try:
+        for key, sig_key, bad_key in (("msg", "partials", "bad_partial"), ("msg_v2", "partials_v2", "bad_partial_v2")):
+            msg = bytes.fromhex(th[key])
+            parts = [bytes.fromhex(p) for p in th[sig_key]]
+            assert all(g.verify_partial(msg, p) == O.REJ_OK for p in parts[:8])
+            assert g.verify_partial(msg, bytes.fromhex(th[bad_key])) != O.REJ_OK
+            assert g.verify_partial(msg, b"\x00") == O.REJ_LENGTH
+        msg = bytes.fromhex(th["msg"])
+        sub = [bytes.fromhex(p) for p in th["recover_subset"]]
+        assert g.recover(msg, sub, th["t"], th["n"]).hex() == th["group_sig"]
+        parts2 = [bytes.fromhex(p) for p in th["partials_v2"]]
+        assert g.recover(bytes.fromhex(th["msg_v2"]), [bytes.fromhex(th["bad_partial_v2"])] + parts2,
+                         th["t"], th["n"]).hex() == th["group_sig_v2"]
+        assert g.recover(msg, sub[:-1], th["t"], th["n"]) is None            # t - 1 good shares
+        assert g.recover(msg, sub[:-1] + [sub[0]], th["t"], th["n"]) is None  # a duplicate counts, collapses
+    finally:
+        g.close()

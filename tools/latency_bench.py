@@ -47,6 +47,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--lat-max", type=int, default=None,
+                    help="latency-path cutover for this run (0 = batch pipeline only; default: the library's)")
     a = ap.parse_args()
     from drand_amd.engine import Engine
 
@@ -60,6 +62,11 @@ def main():
     partials = [bytes.fromhex(p) for p in th["partials"]]
     out = {}
     with Engine(0) as eng:
+        if a.lat_max is not None:
+            eng.set_lat_max(a.lat_max)
+        cur = eng.set_lat_max(0)
+        eng.set_lat_max(cur)
+        out["lat_max"] = cur
         eng.set_public_key(bytes.fromhex(ch["pk"]))
 
         def lone_beacon():
