@@ -757,14 +757,14 @@ static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std:
   HIPCHK(c, c->sel.ensure(t * 4));
   HIPCHK(c, c->idx.ensure(t * 4));
   HIPCHK(c, c->lambdas.ensure(t * 32));
-  HIPCHK(c, c->scratch.ensure(t * 72 * 4));
+  HIPCHK(c, c->scratch.ensure(t * 192 * 4));
   HIPCHK(c, c->out.ensure(96));
   HIPCHK(c, hipMemcpyAsync(c->sel.p, sel.data(), t * 4, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->idx.p, idx.data(), t * 4, hipMemcpyHostToDevice, c->stream));
   blsk::launch_lagrange(c->idx.as<uint32_t>(), (uint32_t)t, c->lambdas.as<uint32_t>(), c->stream);
-  blsk::launch_recover(c->S.as<uint32_t>(), cls.size(), c->s_inf.as<uint8_t>(), c->sel.as<uint32_t>(),
-                       c->lambdas.as<uint32_t>(), (uint32_t)t, c->scratch.as<uint32_t>(), c->out.as<uint8_t>(),
-                       c->stream);
+  blsk::launch_lat_recover(c->S.as<uint32_t>(), cls.size(), c->s_inf.as<uint8_t>(), c->sel.as<uint32_t>(),
+                           c->lambdas.as<uint32_t>(), (uint32_t)t, c->scratch.as<uint32_t>(), c->out.as<uint8_t>(),
+                           c->stream);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(out_sig96, c->out.p, 96, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -161,53 +161,6 @@ __global__ void __launch_bounds__(TPB) k_lagrange(const uint32_t* idx, uint32_t 
   for (int w = 0; w < 8; w++) lambdas[i * 8 + w] = lam.l[w];
 }
 
-DI void st_g2j(uint32_t* buf, size_t k, const g2j& p) {
-  const fp* f[6] = {&p.x.c0, &p.x.c1, &p.y.c0, &p.y.c1, &p.z.c0, &p.z.c1};
-#pragma unroll
-  for (int s = 0; s < 6; s++)
-#pragma unroll
-    for (int w = 0; w < 12; w++) buf[k * 72 + s * 12 + w] = f[s]->l[w];
-}
-
-DI g2j ld_g2j(const uint32_t* buf, size_t k) {
-  g2j p;
-  fp* f[6] = {&p.x.c0, &p.x.c1, &p.y.c0, &p.y.c1, &p.z.c0, &p.z.c1};
-#pragma unroll
-  for (int s = 0; s < 6; s++)
-#pragma unroll
-    for (int w = 0; w < 12; w++) f[s]->l[w] = buf[k * 72 + s * 12 + w];
-  return p;
-}
-
-// [lambda_i] S_sel[i] -> scratch (Jacobian, 72 words each)
-__global__ void __launch_bounds__(TPB) k_recover_mul(const uint32_t* S, size_t n_s, const uint8_t* s_inf,
-                                                     const uint32_t* sel, const uint32_t* lambdas, uint32_t t,
-                                                     uint32_t* scratch) {
-  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
-  if (i >= t) return;
-  const size_t k = sel[i];
-  g2j p;
-  if (s_inf[k]) {
-    p = jac_infinity<fp2>();
-  } else {
-    g2a a = {ld_fp2(S, n_s, k, 0), ld_fp2(S, n_s, k, 2)};
-    uint32_t lam[8];
-#pragma unroll
-    for (int w = 0; w < 8; w++) lam[w] = lambdas[i * 8 + w];
-    p = jac_mul_scalar(jac_from_aff(a), lam);
-  }
-  st_g2j(scratch, i, p);
-}
-
-__global__ void k_recover_sum(const uint32_t* scratch, uint32_t t, uint8_t* out96) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  g2j acc = jac_infinity<fp2>();
-  for (uint32_t i = 0; i < t; i++) acc = jac_add(acc, ld_g2j(scratch, i));
-  uint8_t buf[96];
-  g2_compress(buf, acc);
-  for (int k = 0; k < 96; k++) out96[k] = buf[k];
-}
-
 // ------------------------------------------------------------------ launchers
 void launch_decompress_g1(const uint8_t* in, size_t cnt, uint32_t* tab, uint8_t* inf, uint8_t* cls, hipStream_t st) {
   if (!cnt) return;
@@ -226,11 +179,5 @@ void launch_lagrange(const uint32_t* idx, uint32_t t, uint32_t* lambdas, hipStre
   hipLaunchKernelGGL(k_lagrange, dim3(grid_for(t)), dim3(TPB), 0, st, idx, t, lambdas);
 }
 
-void launch_recover(const uint32_t* S, size_t n_s, const uint8_t* s_inf, const uint32_t* sel, const uint32_t* lambdas,
-                    uint32_t t, uint32_t* scratch, uint8_t* out96, hipStream_t st) {
-  if (!t) return;
-  hipLaunchKernelGGL(k_recover_mul, dim3(grid_for(t)), dim3(TPB), 0, st, S, n_s, s_inf, sel, lambdas, t, scratch);
-  hipLaunchKernelGGL(k_recover_sum, dim3(1), dim3(64), 0, st, scratch, t, out96);
-}
 
 }  // namespace blsk

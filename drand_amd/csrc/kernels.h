@@ -83,8 +83,9 @@ void launch_pubpoly_eval(const uint32_t* commits, const uint8_t* commit_inf, uin
 void launch_lagrange(const uint32_t* idx, uint32_t t, uint32_t* lambdas, hipStream_t st);
 // sum_i [lambda_i] S_i over the selected affine staging entries sel[i] (S in SoA of stride n_s),
 // compressed to 96 bytes
-void launch_recover(const uint32_t* S, size_t n_s, const uint8_t* s_inf, const uint32_t* sel, const uint32_t* lambdas,
-                    uint32_t t, uint32_t* scratch, uint8_t* out96, hipStream_t st);
+// [lambda_i] S_sel[i] summed and compressed (k_latrec.hip, lane form); scratch >= t * 192 words
+void launch_lat_recover(const uint32_t* S, size_t n_s, const uint8_t* s_inf, const uint32_t* sel,
+                        const uint32_t* lambdas, uint32_t t, uint32_t* scratch, uint8_t* out96, hipStream_t st);
 // signatures: out + i*out_stride (+2 index prefix when index >= 0) = compress(sk * H(msg_i))
 void launch_sign(const uint32_t* sk_words, int32_t index, const uint32_t* H, const uint8_t* h_inf, size_t cnt,
                  uint8_t* out, size_t out_stride, hipStream_t st);

@@ -83,11 +83,16 @@ inline F mkF(const V& x, double b) {
 inline double bnd(const F& a) { return a.b; }
 extern uint32_t g_host_lds[LDS_WORDS];
 inline uint32_t* wave_lds() { return g_host_lds; }
+// host op counts (tools/wvtest opcount): dot1..dot6, mulp, sqr2, norm_dup, gcd inversions
+enum { OPC_DOT1 = 0, OPC_MULP = 6, OPC_SQR2, OPC_NORM, OPC_GCD, OPC_N };
+extern unsigned long long g_wv_ops[OPC_N];
+#define WV_COUNT(k) (++g_wv_ops[k])
 #else
 struct F {
   V x;
 };
 #define WV_REQUIRE(v, lim, what) ((void)0)
+#define WV_COUNT(k) ((void)0)
 WVI F mkF(V x, double) { return {x}; }
 WVI double bnd(const F&) { return 0.0; }
 // each wave of a workgroup owns LDS_WORDS words
@@ -205,6 +210,7 @@ WVI V64 fold_halves(V64 x, V64 y) {
 template <int N>
 WVI V dot_body(const V (&a)[N], const V (&b)[N]) {
   static_assert(N >= 1 && N <= MAX_TERMS, "dot terms");
+  WV_COUNT(OPC_DOT1 + N - 1);
 #pragma unroll
   for (int i = 0; i < N; i++) stage_term(i, a[i], b[i], true);
   wsync();
@@ -248,6 +254,7 @@ WV_NOINL V dot6_v(V a0, V b0, V a1, V b1, V a2, V b2, V a3, V b3, V a4, V b4, V 
 }
 // pair product [a0 b0 | a1 b1]
 WV_NOINL V mulp_v(V a, V b) {
+  WV_COUNT(OPC_MULP);
   stage_term(0, a, b, false);
   wsync();
   V64 s[4] = {vsplat64(0), vsplat64(0), vsplat64(0), vsplat64(0)};
@@ -257,6 +264,7 @@ WV_NOINL V mulp_v(V a, V b) {
 }
 // Fp2 square [(a0 + a1)(a0 + D - a1) | (2 a0) a1] as one pair product
 WV_NOINL V sqr2_v(V a) {
+  WV_COUNT(OPC_SQR2);
   const M h0 = in_half0();
   const VP d = pl32_swap(a, a);  // .a = [a0 | a0], .b = [a1 | a1]
   const V u = d.a + sel(h0, d.b, d.a);
@@ -270,6 +278,7 @@ WV_NOINL V sqr2_v(V a) {
 }
 // Fp2 norm a0^2 + a1^2 in both halves: one pair product, halves summed, one reduction
 WV_NOINL V norm_dup_v(V a) {
+  WV_COUNT(OPC_NORM);
   stage_term(0, a, a, false);
   wsync();
   V64 s4[4] = {vsplat64(0), vsplat64(0), vsplat64(0), vsplat64(0)};
@@ -520,6 +529,7 @@ WVI V words_to_limbs(const uint32_t (&w0)[12], const uint32_t (&w1)[12]) {
   return sel((l & 16u) == 0u, v, vsplat(0));
 }
 WVI void gcd_inverse_words(uint32_t (&w)[12]) {
+  WV_COUNT(OPC_GCD);
   bls::u12 y;
   for (int i = 0; i < 12; i++) y[i] = w[i];
   bool conv;

@@ -215,6 +215,7 @@ WVI V lds_ld(const uint32_t* base, const V& off) {
 WVI void lds_st(uint32_t* base, const V& off, const V& x) { WV_LANES base[off.v[l]] = x.v[l]; }
 // global / constant table loads, per-lane index
 WVI V gld(const uint32_t* base, const V& idx) { return lds_ld(base, idx); }
+WVI void gst(uint32_t* base, const V& idx, const V& x) { lds_st(base, idx, x); }
 #undef WV_LANES
 }  // namespace wv
 
@@ -273,6 +274,7 @@ WVI uint32_t lane_val(V x, int l) { return (uint32_t)__builtin_amdgcn_readlane((
 WVI V lds_ld(const uint32_t* base, V off) { return base[off]; }
 WVI void lds_st(uint32_t* base, V off, V x) { base[off] = x; }
 WVI V gld(const uint32_t* base, V idx) { return base[idx]; }
+WVI void gst(uint32_t* base, V idx, V x) { base[idx] = x; }
 }  // namespace wv
 #endif
 

@@ -13,10 +13,11 @@
 #include <string>
 #include <vector>
 
-#include "../drand_amd/csrc/wverify.h"
+#include "../drand_amd/csrc/wrecover.h"
 
 namespace wv {
 uint32_t g_host_lds[LDS_WORDS];
+unsigned long long g_wv_ops[OPC_N];
 }
 namespace bls {
 unsigned long long g_fp_mul_count = 0;
@@ -157,11 +158,81 @@ static int cmd_decompress() {
   return 0;
 }
 
+// opcount: "pk48 msg sig96" (an accepting item) -> JSON op counts per phase of verify_item
+static void ops_line(const char* name, bool last) {
+  static const char* nm[OPC_N] = {"dot1", "dot2", "dot3", "dot4", "dot5", "dot6", "mulp", "sqr2", "norm", "gcd"};
+  printf("\"%s\": {", name);
+  for (int k = 0; k < OPC_N; k++) printf("\"%s\": %llu%s", nm[k], g_wv_ops[k], k + 1 < OPC_N ? ", " : "");
+  printf("}%s", last ? "}\n" : ", ");
+  memset(g_wv_ops, 0, sizeof g_wv_ops);
+}
+static int cmd_opcount() {
+  char a[300], b[4000], c[300];
+  if (scanf("%299s %3999s %299s", a, b, c) != 3) return 2;
+  wv_init();
+  const auto pk = unhex(a), msg = unhex(strcmp(b, "-") ? b : ""), sig = unhex(c);
+  bls::g1a P;
+  bool pinf = false;
+  if (bls::g1_decompress(pk.data(), P, pinf) != bls::REJ_OK) return 3;
+  uint32_t b0[8];
+  msg_b0(msg, b0);
+  memset(g_wv_ops, 0, sizeof g_wv_ops);
+  printf("{");
+  F sx, sy, hx, hy;
+  bool sinf;
+  if (g2_decompress(sig.data(), sx, sy, sinf) != bls::REJ_OK) return 4;
+  ops_line("decompress_subgroup", false);
+  hash_to_g2(b0, hx, hy);
+  ops_line("hash_to_g2", false);
+  MPair pr[2];
+  const bool active[2] = {true, true};
+  pr[0] = mpair(g1_coord(P.x.l), g1_coord(P.y.l), hx, hy);
+  pr[1] = mpair(cst(WC_NEG_G1_X), cst(WC_NEG_G1_Y), sx, sy);
+  ops_line("pair_setup", false);
+  const W12 f0 = miller_loop(pr, active);
+  ops_line("miller", false);
+  const bool ok = final_exp_is_one(f0);
+  ops_line("final_exp", true);
+  return ok ? 0 : 5;
+}
+
+// smul: "sig96 k" (k hex < r) -> compressed [k] S through the x-adic joint multiplication;
+// "sum sig96 sig96" -> compressed S1 + S2
+static int cmd_smul() {
+  static uint32_t tab[15 * POINT_WORDS];
+  char a[300], b[300];
+  while (scanf("%299s %299s", a, b) == 2) {
+    wv_init();
+    const auto sig = unhex(a);
+    F x, y;
+    bool inf;
+    if (g2_decompress(sig.data(), x, y, inf) || inf) {
+      printf("-\n");
+      continue;
+    }
+    uint32_t lam[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const std::string h(b);
+    for (int i = 0; i < (int)h.size(); i++) {  // hex digit i from the right -> bits 4i..4i+3
+      const char c = h[h.size() - 1 - i];
+      const uint32_t v = c <= '9' ? c - '0' : (c | 32) - 'a' + 10;
+      lam[i / 8] |= v << (4 * (i % 8));
+    }
+    const G2J r = g2_mul_lambda(x, y, lam, tab);
+    const V w = g2_compress_words(r);
+    for (int j = 0; j < 24; j++) printf("%08x", lane_val(w, j));
+    printf("\n");
+    fflush(stdout);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 2 && !strcmp(argv[1], "field")) return cmd_field();
   if (argc >= 2 && !strcmp(argv[1], "verify")) return cmd_verify();
   if (argc >= 2 && !strcmp(argv[1], "hash")) return cmd_hash();
   if (argc >= 2 && !strcmp(argv[1], "decompress")) return cmd_decompress();
+  if (argc >= 2 && !strcmp(argv[1], "opcount")) return cmd_opcount();
+  if (argc >= 2 && !strcmp(argv[1], "smul")) return cmd_smul();
   fprintf(stderr, "usage: wvtest field|verify|hash|pair\n");
   return 2;
 }
