@@ -81,11 +81,14 @@ inline F mkF(const V& x, double b) {
   return {x, b};
 }
 inline double bnd(const F& a) { return a.b; }
-extern uint32_t g_host_lds[LDS_WORDS];
-inline uint32_t* wave_lds() { return g_host_lds; }
+// the host runs each wave of a workgroup as a thread (wteam.h): per-wave LDS and op counters
+constexpr int HOST_MAX_WAVES = 8;
+extern uint32_t g_host_lds[HOST_MAX_WAVES][LDS_WORDS];
+extern thread_local int g_host_wave;
+inline uint32_t* wave_lds() { return g_host_lds[g_host_wave]; }
 // host op counts (tools/wvtest opcount): dot1..dot6, mulp, sqr2, norm_dup, gcd inversions
 enum { OPC_DOT1 = 0, OPC_MULP = 6, OPC_SQR2, OPC_NORM, OPC_GCD, OPC_N };
-extern unsigned long long g_wv_ops[OPC_N];
+extern thread_local unsigned long long g_wv_ops[OPC_N];
 #define WV_COUNT(k) (++g_wv_ops[k])
 #else
 struct F {

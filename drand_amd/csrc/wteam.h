@@ -1,0 +1,106 @@
+// Teams of waves for the latency engine: the waves of one workgroup cooperate on ONE item. A wave
+// still computes whole field values (wfield.h, limbs across its lanes); a team splits the independent
+// outputs of an operation (the six coefficients of an Fp12 product, the pieces of a Miller step)
+// across its waves, which exchange the results through the workgroup's LDS.
+//
+//   exchange  a value lives in an LDS slot of 64 words (lane l's word at l); xst / xld
+//   team sync a monotonic LDS counter per team: every wave adds one and waits for gen * n -- waves of
+//             different teams run different code, so the workgroup barrier (which every wave must
+//             reach equally often) only separates phases
+//
+// Host build: each wave of the workgroup is a std::thread running the same function (wvtest), the
+// slots carry their values' bounds, and the counters are std::atomic.
+#pragma once
+#include "wfield.h"
+
+#ifdef WV_HOST
+#include <atomic>
+#include <thread>
+#endif
+
+namespace wv {
+
+#ifndef WV_BLK_SLOTS
+#define WV_BLK_SLOTS 128
+#endif
+constexpr int BLK_SLOTS = WV_BLK_SLOTS;
+constexpr int BLK_CTRS = 8;   // team counters
+constexpr int BLK_WORDS_EXTRA = 64;  // scalar words (verdicts, flags)
+
+#ifdef WV_HOST
+extern uint32_t g_host_blk[BLK_SLOTS * 64 + BLK_WORDS_EXTRA];
+extern double g_host_blk_b[BLK_SLOTS];
+extern std::atomic<uint32_t> g_host_ctr[BLK_CTRS];
+inline uint32_t* blk_base() { return g_host_blk; }
+inline int wave_id() { return g_host_wave; }
+#else
+static __shared__ uint32_t g_wv_blk[BLK_SLOTS * 64 + BLK_WORDS_EXTRA + BLK_CTRS];
+WVI uint32_t* blk_base() { return g_wv_blk; }
+WVI int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+#endif
+
+WVI void xst(int slot, const F& v) {
+  lds_st(blk_base() + slot * 64, lane_id(), v.x);
+#ifdef WV_HOST
+  g_host_blk_b[slot] = v.b;
+#endif
+}
+WVI F xld(int slot) {
+#ifdef WV_HOST
+  return mkF(lds_ld(blk_base() + slot * 64, lane_id()), g_host_blk_b[slot]);
+#else
+  return {lds_ld(blk_base() + slot * 64, lane_id())};
+#endif
+}
+// a wave-uniform scalar word (written by one lane, read by all)
+WVI void xst_word(int i, uint32_t v) {
+  uint32_t* p = blk_base() + BLK_SLOTS * 64 + i;
+#ifdef WV_HOST
+  *p = v;
+#else
+  if (threadIdx.x % 64 == 0) *p = v;
+#endif
+}
+WVI uint32_t xld_word(int i) {
+  const uint32_t* p = blk_base() + BLK_SLOTS * 64 + i;
+#ifdef WV_HOST
+  return *p;
+#else
+  return __builtin_amdgcn_readfirstlane(*(volatile const uint32_t*)p);
+#endif
+}
+
+struct Team {
+  int first, n, id;  // waves first .. first + n - 1; this wave's index in the team
+  int ctr;           // its counter
+  uint32_t gen;      // syncs passed
+};
+WVI Team make_team(int first, int n, int ctr) { return {first, n, wave_id() - first, ctr, 0u}; }
+
+WVI void team_sync(Team& t) {
+  t.gen++;
+  const uint32_t target = t.gen * (uint32_t)t.n;
+#ifdef WV_HOST
+  g_host_ctr[t.ctr].fetch_add(1, std::memory_order_acq_rel);
+  while (g_host_ctr[t.ctr].load(std::memory_order_acquire) < target) std::this_thread::yield();
+#else
+  uint32_t* c = blk_base() + BLK_SLOTS * 64 + BLK_WORDS_EXTRA + t.ctr;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (threadIdx.x % 64 == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+         target)
+    __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#endif
+}
+
+// the workgroup prologue: counters to zero (then a workgroup barrier before any team sync)
+WVI void team_init() {
+#ifdef WV_HOST
+  // the host driver zeroes the counters before it starts the wave threads
+#else
+  if (threadIdx.x < BLK_CTRS) blk_base()[BLK_SLOTS * 64 + BLK_WORDS_EXTRA + threadIdx.x] = 0u;
+#endif
+}
+
+}  // namespace wv

@@ -23,60 +23,58 @@ WVI W12 w12_one() {
   return r;
 }
 
-// xi b for each coefficient (the wrapped terms of a product)
-WVI void w12_xi(const W12& b, F (&xb)[6]) {
-#pragma unroll
-  for (int k = 0; k < 6; k++) xb[k] = mul_xi<1>(b.c[k]);  // b may be a conjugate (odd powers < 4p)
-}
+// Every product below is written per output coefficient (..._c(.., k)), so that the waves of a
+// team (wteam.h) can each compute a share of the six; the whole-value forms loop over k.
 
-// general product
+// general product: c_k = sum_i a_i b'_{k-i}, b'_j = xi b_{j+6} for j < 0
+WVI F w12_mul_c(const W12& a, const W12& b, int k) {
+  auto B = [&](int j) -> F { return j >= 0 ? b.c[j] : mul_xi<1>(b.c[j + 6]); };  // b may be a conjugate
+  return dot(a.c[0], B(k), a.c[1], B(k - 1), a.c[2], B(k - 2), a.c[3], B(k - 3), a.c[4], B(k - 4), a.c[5],
+             B(k - 5));
+}
 WVI W12 w12_mul(const W12& a, const W12& b) {
-  F xb[6];
-  w12_xi(b, xb);
   W12 r;
-  auto B = [&](int j) -> const F& { return j >= 0 ? b.c[j] : xb[j + 6]; };
-#pragma unroll
-  for (int k = 0; k < 6; k++)
-    r.c[k] = dot(a.c[0], B(k), a.c[1], B(k - 1), a.c[2], B(k - 2), a.c[3], B(k - 3), a.c[4], B(k - 4), a.c[5],
-                 B(k - 5));
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) r.c[k] = w12_mul_c(a, b, k);
   return r;
 }
 
 // square: c_k = sum over unordered {i, j}, i + j = k (mod 6, xi when it wraps): a_i a_j, doubled when
 // i != j (the doubled operand 2 a_i sits in the window, a_j or xi a_j is broadcast)
-WVI W12 w12_sqr(const W12& a) {
-  F xa[6], a2[6];
-#pragma unroll
-  for (int k = 0; k < 6; k++) {
-    xa[k] = mul_xi<0>(a.c[k]);
-    a2[k] = dbl(a.c[k]);
+WVI F w12_sqr_c(const W12& a, int k) {
+  auto X = [&](int i) { return mul_xi<0>(a.c[i]); };
+  auto D = [&](int i) { return dbl(a.c[i]); };
+  switch (k) {
+    case 0: return dot(a.c[0], a.c[0], D(1), X(5), D(2), X(4), a.c[3], X(3));  // (0,0) (1,5)x (2,4)x (3,3)x
+    case 1: return dot(D(0), a.c[1], D(2), X(5), D(3), X(4));                  // (0,1) (2,5)x (3,4)x
+    case 2: return dot(D(0), a.c[2], a.c[1], a.c[1], D(3), X(5), a.c[4], X(4));  // (0,2) (1,1) (3,5)x (4,4)x
+    case 3: return dot(D(0), a.c[3], D(1), a.c[2], D(4), X(5));                  // (0,3) (1,2) (4,5)x
+    case 4: return dot(D(0), a.c[4], D(1), a.c[3], a.c[2], a.c[2], a.c[5], X(5));  // (0,4) (1,3) (2,2) (5,5)x
+    default: return dot(D(0), a.c[5], D(1), a.c[4], D(2), a.c[3]);               // (0,5) (1,4) (2,3)
   }
+}
+WVI W12 w12_sqr(const W12& a) {
   W12 r;
-  // k = 0: (0,0) (1,5)x (2,4)x (3,3)x
-  r.c[0] = dot(a.c[0], a.c[0], a2[1], xa[5], a2[2], xa[4], a.c[3], xa[3]);
-  // k = 1: (0,1) (2,5)x (3,4)x
-  r.c[1] = dot(a2[0], a.c[1], a2[2], xa[5], a2[3], xa[4]);
-  // k = 2: (0,2) (1,1) (3,5)x (4,4)x
-  r.c[2] = dot(a2[0], a.c[2], a.c[1], a.c[1], a2[3], xa[5], a.c[4], xa[4]);
-  // k = 3: (0,3) (1,2) (4,5)x
-  r.c[3] = dot(a2[0], a.c[3], a2[1], a.c[2], a2[4], xa[5]);
-  // k = 4: (0,4) (1,3) (2,2) (5,5)x
-  r.c[4] = dot(a2[0], a.c[4], a2[1], a.c[3], a.c[2], a.c[2], a.c[5], xa[5]);
-  // k = 5: (0,5) (1,4) (2,3)
-  r.c[5] = dot(a2[0], a.c[5], a2[1], a.c[4], a2[2], a.c[3]);
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) r.c[k] = w12_sqr_c(a, k);
   return r;
 }
 
 // f * l for a Miller line l = l0 + l2 w^2 + l3 w^3 (tower: l00 + l01 v + l11 v w)
+WVI F w12_mul_line_c(const W12& f, const F& l0, const F& l2, const F& l3, int k) {
+  switch (k) {
+    case 0: return dot(f.c[0], l0, f.c[4], mul_xi<0>(l2), f.c[3], mul_xi<0>(l3));
+    case 1: return dot(f.c[1], l0, f.c[5], mul_xi<0>(l2), f.c[4], mul_xi<0>(l3));
+    case 2: return dot(f.c[2], l0, f.c[0], l2, f.c[5], mul_xi<0>(l3));
+    case 3: return dot(f.c[3], l0, f.c[1], l2, f.c[0], l3);
+    case 4: return dot(f.c[4], l0, f.c[2], l2, f.c[1], l3);
+    default: return dot(f.c[5], l0, f.c[3], l2, f.c[2], l3);
+  }
+}
 WVI W12 w12_mul_line(const W12& f, const F& l0, const F& l2, const F& l3) {
-  const F x2 = mul_xi<0>(l2), x3 = mul_xi<0>(l3);
   W12 r;
-  r.c[0] = dot(f.c[0], l0, f.c[4], x2, f.c[3], x3);
-  r.c[1] = dot(f.c[1], l0, f.c[5], x2, f.c[4], x3);
-  r.c[2] = dot(f.c[2], l0, f.c[0], l2, f.c[5], x3);
-  r.c[3] = dot(f.c[3], l0, f.c[1], l2, f.c[0], l3);
-  r.c[4] = dot(f.c[4], l0, f.c[2], l2, f.c[1], l3);
-  r.c[5] = dot(f.c[5], l0, f.c[3], l2, f.c[2], l3);
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) r.c[k] = w12_mul_line_c(f, l0, l2, l3, k);
   return r;
 }
 
@@ -91,36 +89,42 @@ WVI W12 w12_conj(const W12& a) {
 // negated odd powers as a dot-ready operand is the same thing; conj output bounds are 4 p (neg)
 
 // f^p: c_k -> conj(c_k) gamma1^k
+WVI F w12_frob_c(const W12& a, int k) {
+  return k == 0 ? conj<0>(a.c[0]) : mul2(conj<0>(a.c[k]), cst(WC_FROB1_0 + 2 * k));
+}
 WVI W12 w12_frob(const W12& a) {
   W12 r;
-  r.c[0] = conj<0>(a.c[0]);
-#pragma unroll
-  for (int k = 1; k < 6; k++) r.c[k] = mul2(conj<0>(a.c[k]), cst(WC_FROB1_0 + 2 * k));
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) r.c[k] = w12_frob_c(a, k);
   return r;
 }
 // f^(p^2): c_k -> c_k gamma2^k (gamma2^k in Fp)
+WVI F w12_frob2_c(const W12& a, int k) { return k == 0 ? a.c[0] : mulp(a.c[k], cst(WC_FROB2_0 + 2 * k)); }
 WVI W12 w12_frob2(const W12& a) {
   W12 r;
-  r.c[0] = a.c[0];
-#pragma unroll
-  for (int k = 1; k < 6; k++) r.c[k] = mulp(a.c[k], cst(WC_FROB2_0 + 2 * k));
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) r.c[k] = w12_frob2_c(a, k);
   return r;
 }
 
 // Granger-Scott cyclotomic square (tower.h fp12_cyclotomic_sqr) with z0..z5 = c0, c3, c1, c4, c2, c5
 // (w-powers 0, 3, 1, 4, 2, 5): each output is one dot, the 3 t - 2 z / 3 t + 2 z fix-ups as terms
 // against the Montgomery constants -2, 2
-WVI W12 w12_cyc_sqr(const W12& f) {
+WVI F w12_cyc_sqr_c(const W12& f, int k) {
   const F &z0 = f.c[0], &z1 = f.c[3], &z2 = f.c[1], &z3 = f.c[4], &z4 = f.c[2], &z5 = f.c[5];
-  const F m2 = cst(WC_NEG2), p2 = cst(WC_POS2);
-  const F x1 = mul_xi<0>(z1), x3 = mul_xi<0>(z3), x5 = mul_xi<0>(z5);
+  switch (k) {
+    case 0: return dot(z0, mul_small<3>(z0), z1, mul_small<3>(mul_xi<0>(z1)), z0, cst(WC_NEG2));  // z0' = 3 (z0^2 + xi z1^2) - 2 z0
+    case 3: return dot(z0, mul_small<6>(z1), z1, cst(WC_POS2));                                  // z1' = 6 z0 z1 + 2 z1
+    case 2: return dot(z2, mul_small<3>(z2), z3, mul_small<3>(mul_xi<0>(z3)), z4, cst(WC_NEG2));  // z4' = 3 (z2^2 + xi z3^2) - 2 z4
+    case 5: return dot(z2, mul_small<6>(z3), z5, cst(WC_POS2));                                  // z5' = 6 z2 z3 + 2 z5
+    case 1: return dot(z4, mul_small<6>(mul_xi<0>(z5)), z2, cst(WC_POS2));                       // z2' = 6 xi z4 z5 + 2 z2
+    default: return dot(z4, mul_small<3>(z4), z5, mul_small<3>(mul_xi<0>(z5)), z3, cst(WC_NEG2));  // z3' = 3 (z4^2 + xi z5^2) - 2 z3
+  }
+}
+WVI W12 w12_cyc_sqr(const W12& f) {
   W12 r;
-  r.c[0] = dot(z0, mul_small<3>(z0), z1, mul_small<3>(x1), z0, m2);  // z0' = 3 (z0^2 + xi z1^2) - 2 z0
-  r.c[3] = dot(z0, mul_small<6>(z1), z1, p2);                          // z1' = 6 z0 z1 + 2 z1
-  r.c[2] = dot(z2, mul_small<3>(z2), z3, mul_small<3>(x3), z4, m2);  // z4' = 3 (z2^2 + xi z3^2) - 2 z4
-  r.c[5] = dot(z2, mul_small<6>(z3), z5, p2);                          // z5' = 6 z2 z3 + 2 z5
-  r.c[1] = dot(z4, mul_small<6>(x5), z2, p2);                          // z2' = 6 xi z4 z5 + 2 z2
-  r.c[4] = dot(z4, mul_small<3>(z4), z5, mul_small<3>(x5), z3, m2);  // z3' = 3 (z4^2 + xi z5^2) - 2 z3
+#pragma unroll 1
+  for (int k = 0; k < 6; k++) r.c[k] = w12_cyc_sqr_c(f, k);
   return r;
 }
 

@@ -73,7 +73,10 @@ def test_decompress_matches_oracle(wvtest, golden):
         assert line == want, s
 
 
-def test_verify_kat_and_chain(wvtest, golden):
+@pytest.mark.parametrize("cmd", ["verify", "tverify"])
+def test_verify_kat_and_chain(wvtest, golden, cmd):
+    """verify = one wave (wverify.h); tverify = the four-wave team of the device kernels (wvteam.h),
+    one host thread per wave"""
     kat = golden["kat"]
     ch = golden["chained"]
     seed = bytes.fromhex(ch["genesis_seed"])
@@ -85,11 +88,12 @@ def test_verify_kat_and_chain(wvtest, golden):
     # negative controls: the KAT signature on another message, a beacon under the wrong round
     lines.append("%s %s %s" % (kat["pk"], "00" + kat["msg"], kat["sig"]))
     lines.append("%s %s %s" % (ch["pk"], O.message(beacons[0]["round"] + 1, seed).hex(), beacons[0]["sig"]))
-    assert run(wvtest, "verify", lines) == ["0"] * 4 + ["7", "7"]
+    assert run(wvtest, cmd, lines) == ["0"] * 4 + ["7", "7"]
 
 
 @pytest.mark.slow
-def test_verify_mixed_golden_classes(wvtest, golden):
+@pytest.mark.parametrize("cmd", ["verify", "tverify"])
+def test_verify_mixed_golden_classes(wvtest, golden, cmd):
     """Every reject class of the mixed golden batch (configs[4] classes, chained messages)."""
     m = golden["mixed"]
     seed = bytes.fromhex(m["genesis_seed"])
@@ -98,4 +102,4 @@ def test_verify_mixed_golden_classes(wvtest, golden):
     for i, s in enumerate(sigs):
         prev = seed if i == 0 else sigs[i - 1]
         lines.append("%s %s %s" % (m["pk"], O.message(i + 1, prev).hex(), s.hex()))
-    assert [int(x) for x in run(wvtest, "verify", lines)] == m["expect_class"]
+    assert [int(x) for x in run(wvtest, cmd, lines)] == m["expect_class"]

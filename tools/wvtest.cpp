@@ -14,10 +14,17 @@
 #include <vector>
 
 #include "../drand_amd/csrc/wrecover.h"
+#include "../drand_amd/csrc/wvteam.h"
+
+#include <thread>
 
 namespace wv {
-uint32_t g_host_lds[LDS_WORDS];
-unsigned long long g_wv_ops[OPC_N];
+uint32_t g_host_lds[HOST_MAX_WAVES][LDS_WORDS];
+thread_local int g_host_wave = 0;
+thread_local unsigned long long g_wv_ops[OPC_N];
+uint32_t g_host_blk[BLK_SLOTS * 64 + BLK_WORDS_EXTRA];
+double g_host_blk_b[BLK_SLOTS];
+std::atomic<uint32_t> g_host_ctr[BLK_CTRS];
 }
 namespace bls {
 unsigned long long g_fp_mul_count = 0;
@@ -116,6 +123,43 @@ static int cmd_verify() {
     bool sinf;
     const int cls = sig.size() == 96 ? verify_item(sig.data(), b0, P.x.l, P.y.l, pinf, sx, sy, sinf) : bls::REJ_LENGTH;
     printf("%d\n", cls);
+    fflush(stdout);
+  }
+  return 0;
+}
+
+// tverify: as verify, by the four-wave team (wvteam.h), one host thread per wave
+static int cmd_tverify() {
+  char a[300], b[4000], c[300];
+  while (scanf("%299s %3999s %299s", a, b, c) == 3) {
+    const auto pk = unhex(a), msg = unhex(strcmp(b, "-") ? b : ""), sig = unhex(c);
+    bls::g1a P;
+    bool pinf = false;
+    if (bls::g1_decompress(pk.data(), P, pinf) != bls::REJ_OK) {
+      printf("-1\n");
+      continue;
+    }
+    if (sig.size() != 96) {
+      printf("%d\n", bls::REJ_LENGTH);
+      continue;
+    }
+    uint32_t b0[8];
+    msg_b0(msg, b0);
+    for (auto& ctr : g_host_ctr) ctr.store(0);
+    int cls[4];
+    std::thread th[4];
+    for (int w = 0; w < 4; w++)
+      th[w] = std::thread([&, w]() {
+        g_host_wave = w;
+        wv_init();
+        F sx, sy;
+        bool sinf = false;
+        cls[w] = verify_team(sig.data(), b0, P.x.l, P.y.l, pinf, sx, sy, sinf);
+      });
+    for (auto& t : th) t.join();
+    for (int w = 1; w < 4; w++)
+      if (cls[w] != cls[0]) fprintf(stderr, "waves disagree: %d vs %d\n", cls[w], cls[0]), abort();
+    printf("%d\n", cls[0]);
     fflush(stdout);
   }
   return 0;
@@ -229,6 +273,7 @@ static int cmd_smul() {
 int main(int argc, char** argv) {
   if (argc >= 2 && !strcmp(argv[1], "field")) return cmd_field();
   if (argc >= 2 && !strcmp(argv[1], "verify")) return cmd_verify();
+  if (argc >= 2 && !strcmp(argv[1], "tverify")) return cmd_tverify();
   if (argc >= 2 && !strcmp(argv[1], "hash")) return cmd_hash();
   if (argc >= 2 && !strcmp(argv[1], "decompress")) return cmd_decompress();
   if (argc >= 2 && !strcmp(argv[1], "opcount")) return cmd_opcount();
