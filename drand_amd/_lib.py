@@ -79,7 +79,7 @@ SIGNATURES = {
     "blsv_test_pairing": (ctypes.c_int, [vp, u32p, u32p, sz, u32p]),
     "blsv_test_hash_to_g2": (ctypes.c_int, [vp, u8p, u32p, sz, u32p, u8p]),
     "blsv_test_final_exp": (ctypes.c_int, [vp, u32p, sz, u32p, u32p]),
-    "blsv_test_set_lat_max": (sz, [vp, sz]),
+    "blsv_set_lat_max": (sz, [vp, sz]),
 }
 
 _lib = None

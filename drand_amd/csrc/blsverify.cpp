@@ -979,13 +979,15 @@ int blsv_profile_read(blsv_ctx* c, double* ms, uint64_t* launches, uint64_t* ite
   return ST_N;
 }
 
-// ------------------------------------------------------------------ testing hooks
-size_t blsv_test_set_lat_max(blsv_ctx* c, size_t lat_max) {
+// latency-path cutover (include/blsverify.h latency contract)
+size_t blsv_set_lat_max(blsv_ctx* c, size_t lat_max) {
   if (!c) return 0;
   const size_t prev = c->lat_max;
   c->lat_max = lat_max;
   return prev;
 }
+
+// ------------------------------------------------------------------ testing hooks
 
 int blsv_test_fp_mul(blsv_ctx* c, const uint32_t* a, const uint32_t* b, size_t n, uint32_t* out) {
   if (!c || (n && (!a || !b || !out))) return BLSV_EINVAL;

@@ -307,7 +307,7 @@ class Engine:
     # ------------------------------------------------------------------ testing hooks
     def set_lat_max(self, n):
         """Batches of at most n items take the latency path (one wave per item); returns the old cutover."""
-        return self.lib.blsv_test_set_lat_max(self._h, int(n))
+        return self.lib.blsv_set_lat_max(self._h, int(n))
 
     def test_fp_mul(self, a_limbs, b_limbs):
         n = len(a_limbs) // 12

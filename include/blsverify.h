@@ -20,6 +20,21 @@
  *    rejected item, UINT64_MAX when every item verified.
  *  - A context owns one HIP stream and is not thread-safe; use one context per calling thread
  *    (the Go adapter serialises with a mutex or keeps a pool).
+ *
+ * Latency contract (single-item and small callers: client.Get's per-round verify,
+ * client/verify.go:185-207; the gossip validator, lp2p/client/validator.go:64; per-packet
+ * VerifyPartial, chain/beacon/node.go:112,125; identity checks, key/keys.go:60-63)
+ *  - A call with at most lat_max items (blsv_set_lat_max, default 2048) runs on the LATENCY path: one
+ *    workgroup of four waves per item, every limb of a field element in its own lane
+ *    (drand_amd/csrc/k_lat.hip). Measured on MI355X (profiles/r03_cabi_smoke.txt, this ABI from
+ *    plain C, warm): one VerifyRecovered 3.8 ms; blsv_aggregate of an n = 64 / t = 33 round (64
+ *    VerifyPartial + Recover + VerifyRecovered) 10.0 ms. Up to ~512 items the time stays ~4 ms
+ *    (every item has its own CU), then grows ~8.5 ms per further 1024 items
+ *    (profiles/r03_latency_sweep.json).
+ *  - Larger calls run on the BATCH pipeline (one lane per item, staged kernels): ~19 ms floor, then
+ *    ~0.5 us per item (about 2 M items/s). Both paths give identical verdicts, reject classes and
+ *    recovered bytes (tests/test_gpu_lat.py runs the same vectors through both).
+ *  - The first call on a context also pays allocation and module load (~10-250 ms).
  */
 #ifndef DRAND_AMD_BLSVERIFY_H
 #define DRAND_AMD_BLSVERIFY_H
@@ -215,6 +230,13 @@ int blsv_generate_chained_dev(blsv_ctx* ctx, const uint8_t* sk32, uint64_t first
 
 /* Wait for the context stream. */
 int blsv_synchronize(blsv_ctx* ctx);
+
+/*
+ * Latency-path cutover (see the latency contract above): calls with 1..lat_max items take the latency
+ * path, larger ones the batch pipeline; 0 = batch pipeline only. The default is the BLSV_LAT_MAX
+ * environment variable, else 2048 (where the two paths cross on MI355X). Returns the previous value.
+ */
+size_t blsv_set_lat_max(blsv_ctx* ctx, size_t lat_max);
 
 #ifdef __cplusplus
 }

@@ -34,14 +34,6 @@ int blsv_test_hash_to_g2(blsv_ctx* ctx, const uint8_t* msgs, const uint32_t* msg
                          uint8_t* inf);
 
 /*
- * Batches of at most lat_max items run on the latency path (one wave per item, drand_amd/csrc/
- * k_lat.hip); larger ones on the batch pipeline. The default comes from the BLSV_LAT_MAX environment
- * variable (else the built-in cutover); tests set it to run the same vectors through both paths.
- * Returns the previous value.
- */
-size_t blsv_test_set_lat_max(blsv_ctx* ctx, size_t lat_max);
-
-/*
  * Stage timing for bench.py's roofline: when enabled, every stage launch (0 hash, 1 decompress,
  * 2 miller, 3 final_exp, 4 finish) is bracketed by HIP events on its launch stream.
  * blsv_profile_read waits for the recorded events, writes per-stage summed milliseconds, launch

@@ -109,3 +109,80 @@ def test_host_build_inversion_matches_exponentiation(opcount_bin):
     r = subprocess.run([opcount_bin, "invfuzz", "20000"], capture_output=True, text=True)
     out = json.loads(r.stdout)
     assert r.returncode == 0 and out["bad"] == 0 and out["unconverged"] == 0 and out["structured"] > 2000, out
+
+
+def _split_top(args):
+    out, depth, cur = [], 0, ""
+    for ch in args:
+        if ch in "([{":
+            depth += 1
+        elif ch in ")]}":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def header_prototypes():
+    """name -> list of parameter types of every blsv_* function in include/*.h"""
+    protos = {}
+    for h in ("blsverify.h", "blsverify_testing.h"):
+        txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", h)).read(), flags=re.S)
+        for m in re.finditer(r"\b(blsv_\w+)\s*\(([^;{]*?)\)\s*;", txt):
+            params = _split_top(m.group(2))
+            protos[m.group(1)] = [] if params == ["void"] else [re.sub(r"\s*\b\w+$", "", p) if "*" not in p.split()[-1]
+                                                                else p for p in params]
+    return protos
+
+
+def _arg_kind(expr):
+    m = re.match(r"C\.(size_t|uint64_t|int32_t|uint32_t|int|uint8_t)\(", expr)
+    if m:
+        return m.group(1)
+    if re.match(r"(ptr\(|&|e\.ctx$|ctx$|nil$|unsafe\.Pointer\(|\(\*C\.)", expr):
+        return "ptr"
+    return None
+
+
+def _param_kind(ptype):
+    if "*" in ptype:
+        return "ptr"
+    for k in ("size_t", "uint64_t", "int32_t", "uint32_t", "uint8_t", "int"):
+        if re.search(r"\b%s\b" % k, ptype):
+            return k
+    return None
+
+
+def test_integration_cgo_calls_match_header():
+    """Compile-shape check of the Go adapter in INTEGRATION.md against include/*.h: every C.blsv_*
+    call names a declared function with the declared number of arguments, each scalar argument is
+    converted to the declared C type (C.size_t(...) for size_t, ...) and each pointer parameter gets
+    a pointer expression; every C.BLSV_* constant is defined by the header."""
+    protos = header_prototypes()
+    md = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    go = "\n".join(re.findall(r"```go\n(.*?)```", md, flags=re.S))
+    calls = 0
+    for m in re.finditer(r"\bC\.(blsv_\w+)\(", go):
+        name = m.group(1)
+        assert name in protos, "INTEGRATION.md calls undeclared %s" % name
+        depth, i = 1, m.end()
+        while depth:
+            depth += {"(": 1, ")": -1}.get(go[i], 0)
+            i += 1
+        args = _split_top(go[m.end():i - 1])
+        params = protos[name]
+        assert len(args) == len(params), "%s: %d args, header declares %d" % (name, len(args), len(params))
+        for a, p in zip(args, params):
+            ak, pk = _arg_kind(a), _param_kind(p)
+            if ak is not None and pk is not None:
+                assert ak == pk, "%s: argument %r for parameter %r" % (name, a, p)
+        calls += 1
+    assert calls >= 10
+    hdr = open(os.path.join(ROOT, "include", "blsverify.h")).read()
+    for c in set(re.findall(r"\bC\.(BLSV_\w*[A-Z0-9])\b", go)):
+        assert re.search(r"\b%s\b\s*=|#define\s+%s\b" % (c, c), hdr), c

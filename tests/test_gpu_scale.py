@@ -160,3 +160,73 @@ def test_sharded_slices_with_phase_match_whole(engine, golden):
             got += [(bm[i // 64] >> (i % 64)) & 1 == 1 for i in range(c)]
         assert got == ok_whole
         assert not got[cut] and (not got[cut + 1] or (cut + 1) % seg == 0)
+
+
+def test_configs3_shard_7_of_8_full_size(engine, golden, C):
+    """BASELINE.json configs[3] at full per-GPU size: rank 7 of a 100,000,000-round history split 8
+    ways (12,500,000 rounds, first round 87,500,001, seg_phase 32 -- the shard starts mid-segment and
+    is not 64-aligned), generated on the device from its segment's start and verified through
+    shard.segmented_slice / local_seeds / verify_chained_dev exactly as bench.py --total-rounds does
+    per rank. All rounds accept; the C oracle re-verifies the halo segment (true previous signature
+    of the first round, generated by rank 6's range), the last segment and samples in between; a
+    corrupted halo must reject the shard's first round and only it; a corrupted signature inside the
+    shard rejects it and its successor (client/verify.go:146-163 linkage)."""
+    import torch
+
+    from drand_amd import shard
+
+    total, world, rank, seg = 100_000_000, 8, 7, 64
+    sl = shard.segmented_slice(total, world, rank, seg)
+    n = sl.shard.count
+    assert n == 12_500_000 and sl.shard.first_round == 87_500_001 and sl.phase == 32
+    ch = golden["chained"]
+    pk48 = bytes.fromhex(ch["pk"])
+    engine.set_public_key(pk48)
+    sk32 = int(ch["sk"], 16).to_bytes(32, "big")
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(0xC0F3)
+    seg_seeds = torch.randint(0, 256, (sl.n_seg, 96), dtype=torch.uint8, device="cuda:0", generator=g)
+    gen_sigs = torch.empty((sl.gen_count, 96), dtype=torch.uint8, device="cuda:0")
+    engine.generate_chained_dev(sk32, sl.gen_start + 1, seg, seg_seeds.data_ptr(), 96, gen_sigs.data_ptr(),
+                                sl.gen_count)
+    torch.cuda.synchronize()
+    loc = shard.local_seeds(sl, seg_seeds, gen_sigs)
+    mine = gen_sigs[sl.phase:sl.phase + n]
+    words = (n + 63) // 64
+    bitmap = torch.zeros(words, dtype=torch.int64, device="cuda:0")
+    fb = torch.empty(1, dtype=torch.int64, device="cuda:0")
+
+    import numpy as np
+
+    def verify():
+        bitmap.zero_()
+        engine.verify_chained_dev(sl.shard.first_round, seg, loc.data_ptr(), 96, mine.data_ptr(), n,
+                                  bitmap.data_ptr(), fb.data_ptr(), None, None, seg_phase=sl.phase)
+        torch.cuda.synchronize()
+        bits = np.unpackbits(bitmap.cpu().numpy().view(np.uint8), bitorder="little")[:n]
+        return set(np.flatnonzero(bits == 0).tolist()), int(fb.item()) & NONE
+
+    rejected, f = verify()
+    assert not rejected and f == NONE
+    # the C oracle on the halo segment (the 32 rounds up to the first segment boundary), samples in
+    # between and the last rounds
+    host = mine.cpu().numpy()
+    halo = bytes(loc[0].cpu().numpy())
+    first = sl.shard.first_round
+    head = seg - sl.phase
+    assert C.verify_chained(pk48, first, halo, host[:head].tobytes()) == [0] * head
+    for lo in (head + seg * 1000 + 5, head + seg * 97_000 + 10, n - 8):  # none at a segment start
+        assert C.verify_chained(pk48, first + lo, bytes(host[lo - 1]), host[lo:lo + 8].tobytes()) == [0] * 8
+    # negative controls: a corrupted halo rejects the shard's first round and only it ...
+    bad_halo = halo[:50] + bytes([halo[50] ^ 1]) + halo[51:]
+    assert C.verify_chained(pk48, first, bad_halo, host[:1].tobytes()) == [7]
+    loc[0, 50] ^= 1
+    rejected, f = verify()
+    loc[0, 50] ^= 1
+    assert rejected == {0} and f == first
+    # ... and a corrupted signature inside the shard rejects it and its successor
+    i = 6_250_001  # (i + phase) % seg = 49: the successor is in the same segment
+    mine[i, 60] ^= 0x10
+    rejected, f = verify()
+    mine[i, 60] ^= 0x10
+    assert rejected == {i, i + 1} and f == first + i

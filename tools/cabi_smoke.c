@@ -179,12 +179,29 @@ int main(int argc, char** argv) {
   check(status == BLSV_AGG_OK_V2 && v2ok && memcmp(gsig, get("group_sig", 0)->data, 96) == 0 &&
             memcmp(gsig2, get("group_sig_v2", 0)->data, 96) == 0,
         "aggregate_round: V1 + V2 group signatures byte-exact");
-  printf("INFO aggregate_round n=%d t=%d (V1+V2, %d partials): %.1f ms\n", gn, t, 2 * np, agg_ms);
+  printf("INFO aggregate_round n=%d t=%d (V1+V2, %d partials): %.1f ms (first call)\n", gn, t, 2 * np, agg_ms);
+  /* warm: the fused V1 round (VerifyPartial x n + Recover + VerifyRecovered) and the V1+V2 round */
+  double best_agg = 1e30, best_round = 1e30;
+  for (int r = 0; r < 5; r++) {
+    uint8_t gok = 0;
+    double a = now_ms();
+    RC(blsv_aggregate(ctx, msg1->data, msg1->len, p1, 98, (size_t)np, (size_t)t, (size_t)gn, okv, rcls, gsig, &gok));
+    double d = now_ms() - a;
+    best_agg = d < best_agg ? d : best_agg;
+    check(gok && memcmp(gsig, get("group_sig", 0)->data, 96) == 0, "aggregate (warm): group signature byte-exact");
+    a = now_ms();
+    RC(blsv_aggregate_round(ctx, msg1->data, msg1->len, p1, (size_t)np, msg2->data, msg2->len, p2, (size_t)np, 98,
+                            (size_t)t, (size_t)gn, okv, okv2, gsig, gsig2, &status, &v2ok));
+    d = now_ms() - a;
+    best_round = d < best_round ? d : best_round;
+  }
+  printf("INFO warm fused round n=%d t=%d (blsv_aggregate, %d partials): %.2f ms\n", gn, t, np, best_agg);
+  printf("INFO warm aggregate_round V1+V2 (%d partials): %.2f ms\n", 2 * np, best_round);
 
-  /* 5. lone VerifyRecovered latency (best of 3) */
+  /* 5. lone VerifyRecovered latency (warm, best of 5) */
   RC(blsv_set_group(ctx, pk->data, 1, 1));
   double best = 1e30;
-  for (int r = 0; r < 3; r++) {
+  for (int r = 0; r < 5; r++) {
     double a = now_ms();
     RC(blsv_verify_chained(ctx, 1, seed->data, seed->len, sigs, 1, bm, &fb, cls));
     double d = now_ms() - a;

@@ -6,7 +6,8 @@ VerifyRecovered of the group signature. Reports the median wall-clock latency pe
 
 configs[4] mixed batch: a device-generated 1M-round chained history (bench.py's layout: segments of
 64 rounds, golden key) with a seeded 0.1 % of signatures corrupted on device (bit flip in x, cleared
-compression flag, infinity encoding, x >= p, a valid signature of another round). The verdict
+compression flag, infinity encoding, x >= p, a valid signature of another round, an on-curve point
+outside G2 and an x with no point on the curve -- the last two taken from the golden mixed batch). The verdict
 bitmap must equal the expectation exactly: a corrupted sig_i rejects round i and, inside its
 segment, round i + 1 (whose message hashes the corrupted bytes); first_bad = the minimum. Reports
 beacons/s over the mixed batch.
@@ -23,7 +24,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
+sys.path.insert(0, ROOT)  # bench.host_cores, oracle.c_oracle (CPU baseline leg)
 
 
 def threshold_round(eng, th, reps):
@@ -53,10 +54,43 @@ def threshold_round(eng, th, reps):
     return {"n": th["n"], "t": th["t"], "median_ms_per_round": round(statistics.median(lat), 3),
             "min_ms": round(min(lat), 3), "reps": reps, "bit_exact_group_sig": True,
             "three_calls": "verify_partials + recover + verify_messages",
-            "fused_blsv_aggregate_median_ms": round(statistics.median(fused), 3)}
+            "fused_blsv_aggregate_median_ms": round(statistics.median(fused), 3),
+            "cpu_baseline": threshold_round_cpu(th, reps=3)}
 
 
-def mixed_batch(eng, g, n, seg, steps):
+def threshold_round_cpu(th, reps):
+    """The same round on the host: the C oracle (oracle/c/bls_oracle.c, kind "port") with the 64
+    VerifyPartial calls (node.go:112, PubPoly.Eval per call as kyber tbls does) spread over all usable
+    cores, then tbls.Recover (which re-verifies shares one by one until t are valid, as kyber's does)
+    and VerifyRecovered on one core. Bench-side baseline only; never on the product path."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from bench import host_cores
+    from oracle import c_oracle  # CPU baseline leg only
+
+    cores, host = host_cores()
+    commits = [bytes.fromhex(c) for c in th["commits"]]
+    msg = bytes.fromhex(th["msg"])
+    partials = [bytes.fromhex(p) for p in th["partials"]]
+    sub = [bytes.fromhex(p) for p in th["recover_subset"]]
+    pk = commits[0]
+    g = c_oracle.Group(commits)
+    lat = []
+    with ThreadPoolExecutor(cores) as ex:
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            cls = list(ex.map(lambda p: g.verify_partial(msg, p), partials))
+            sig = g.recover(msg, sub, th["t"], th["n"])
+            ok = c_oracle.verify(pk, msg, sig)
+            lat.append((time.perf_counter() - t0) * 1e3)
+            assert cls == [0] * len(partials) and sig.hex() == th["group_sig"] and ok == 0
+    g.close()
+    return {"median_ms_per_round": round(statistics.median(lat), 1), "cores": cores, "kind": "port",
+            "host": host, "steps": "64 VerifyPartial over %d threads + Recover(33, re-verifying) + VerifyRecovered"
+            % cores}
+
+
+def mixed_batch(eng, g, mixed, n, seg, steps):
     import torch
     dev = torch.device("cuda", 0)
     sk32 = int(g["sk"], 16).to_bytes(32, "big")
@@ -79,10 +113,17 @@ def mixed_batch(eng, g, n, seg, steps):
     s2 = sigs.view(n, 96)
     p_bytes = bytes.fromhex("1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab")
     p_t = torch.tensor(list(p_bytes), dtype=torch.uint8, device=dev)
+    def golden_of_class(c):  # a signature of the golden mixed batch with reject class c
+        return torch.tensor(list(bytes.fromhex(mixed["sigs"][mixed["expect_class"].index(c)])), dtype=torch.uint8,
+                            device=dev)
+
+    not_in_g2, not_on_curve = golden_of_class(6), golden_of_class(5)
     kinds = {}
+    kind_of = {}
     for j, i in enumerate(idx.tolist()):
-        kind = j % 5
+        kind = j % 7
         kinds[kind] = kinds.get(kind, 0) + 1
+        kind_of[i] = kind
         if kind == 0:                                       # bit flip in x
             s2[i, 60] ^= 0x10
         elif kind == 1:                                     # compression flag cleared
@@ -92,14 +133,33 @@ def mixed_batch(eng, g, n, seg, steps):
             s2[i, 0] = 0xC0
         elif kind == 3:                                     # x.c0 = p (non-canonical)
             s2[i, 48:96] = p_t
-        else:                                               # a valid signature of another round
+        elif kind == 4:                                     # a valid signature of another round
             s2[i] = s2[(i + 7) % n].clone()
+        elif kind == 5:                                     # on the curve, outside G2 (subgroup check)
+            s2[i] = not_in_g2
+        else:                                               # x with no curve point
+            s2[i] = not_on_curve
     torch.cuda.synchronize(dev)
     bad = set(idx.tolist())
     expect_bad = set(bad)
     for i in bad:
         if i + 1 < n and (i + 1) % seg != 0:
             expect_bad.add(i + 1)
+
+    cls = torch.empty(n, dtype=torch.uint8, device=dev)
+    eng.verify_chained_dev(1, seg, seeds.data_ptr(), 32, sigs.data_ptr(), n, bitmap.data_ptr(),
+                           first_bad.data_ptr(), cls.data_ptr(), sp)
+    torch.cuda.synchronize(dev)
+    # reject class per injected kind (include/blsverify.h BLSV_REJ_*); a bit flip lands on any class
+    want_cls = {1: 2, 2: 7, 3: 4, 4: 7, 5: 6, 6: 5}
+    cl = cls.cpu().numpy()
+    for i, kind in kind_of.items():
+        if kind in want_cls and not (kind == 4 and (i + 7) % n < i):  # a wrapped copy may be corrupted itself
+            assert cl[i] == want_cls[kind], (i, kind, int(cl[i]))
+        else:
+            assert cl[i] != 0, (i, kind)
+    for i in expect_bad - bad:
+        assert cl[i] == 7, (i, int(cl[i]))  # the successor's message hashes the corrupted bytes
 
     def step():
         eng.verify_chained_dev(1, seg, seeds.data_ptr(), 32, sigs.data_ptr(), n, bitmap.data_ptr(),
@@ -121,7 +181,7 @@ def mixed_batch(eng, g, n, seg, steps):
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     return {"n": n, "segment_len": seg, "corrupted": k, "rejected": len(expect_bad), "kinds": kinds,
-            "bitmap_exact": True, "first_bad_round": fb, "beacons_per_s": round(n * steps / dt, 1),
+            "bitmap_exact": True, "reject_classes_exact": True, "first_bad_round": fb, "beacons_per_s": round(n * steps / dt, 1),
             "ms_per_batch": round(dt * 1e3 / steps, 3)}
 
 
@@ -185,7 +245,8 @@ def main():
         golden = json.load(f)
     eng = Engine(0)
     out = {"configs[2]_threshold_round": threshold_round(eng, golden["threshold"], args.reps),
-           "configs[4]_mixed_batch": mixed_batch(eng, golden["chained"], args.n, args.seg_len, args.steps)}
+           "configs[4]_mixed_batch": mixed_batch(eng, golden["chained"], golden["mixed"], args.n, args.seg_len,
+                                                  args.steps)}
     if args.partials_n:
         out["configs[2]_partials_many_rounds"] = partials_many_rounds(eng, golden, args.partials_n)
     if args.store_n:

@@ -9,7 +9,10 @@ Each is the median wall clock over `reps` calls from the host API, plus the per-
 one call (HIP events on the launch stream, blsv_profile_*). Inputs are the committed golden vectors
 (tests/golden/golden.json); every result is checked against them.
 
-usage: python tools/latency_bench.py [--reps 20] [--out profiles/r02_latency.json]
+--sweep N1,N2,..: also time blsv_verify_messages of N distinct device-signed messages through the
+latency path and through the batch pipeline (the BLSV_LAT_MAX cutover is where they cross).
+
+usage: python tools/latency_bench.py [--reps 20] [--out profiles/r02_latency.json] [--sweep 64,512]
 """
 import argparse
 import json
@@ -49,6 +52,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--lat-max", type=int, default=None,
                     help="latency-path cutover for this run (0 = batch pipeline only; default: the library's)")
+    ap.add_argument("--sweep", default="", help="batch sizes for the latency-vs-batch crossover")
     a = ap.parse_args()
     from drand_amd.engine import Engine
 
@@ -98,6 +102,29 @@ def main():
 
         med, mn = timed(agg, a.reps)
         out["aggregate_round_n64_t33"] = {"median_ms": med, "min_ms": mn, "stages_ms": stages(eng, agg)}
+        if a.sweep:
+            import hashlib
+            sk32 = int(ch["sk"], 16).to_bytes(32, "big")
+            pk = bytes.fromhex(ch["pk"])
+            cur = eng.set_lat_max(0)
+            eng.set_lat_max(cur)
+            sweep = []
+            for n in [int(x) for x in a.sweep.split(",")]:
+                msgs = [hashlib.sha256(b"sweep %d" % i).digest() for i in range(n)]
+                sigs = eng.sign(sk32, msgs)
+                row = {"n": n}
+                for name, lm in (("lat_ms", 1 << 40), ("batch_ms", 0)):
+                    eng.set_lat_max(lm)
+
+                    def call():
+                        r = eng.verify_messages(msgs, sigs, pk48=pk)
+                        assert all(r.ok)
+
+                    row[name] = timed(call, 3)[0]
+                sweep.append(row)
+                print(json.dumps(row), flush=True)
+            eng.set_lat_max(cur)
+            out["cutover_sweep"] = sweep
     line = json.dumps(out)
     print(line)
     if a.out:
