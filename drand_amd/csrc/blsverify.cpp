@@ -126,7 +126,7 @@ static int ensure_workspace(blsv_ctx* c, size_t cnt) {
   HIPCHK(c, c->F.ensure(want * blsk::F_WORDS * 4));
   HIPCHK(c, c->FW.ensure(3 * want * blsk::F_WORDS * 4));
   HIPCHK(c, c->LN.ensure(std::max(std::min(want, kLineSub) * blsk::MILLER_LINE_WORDS,
-                                   blsk::TRI_PARK_WORDS(want)) * 4));  // LN doubles as the 3-lane park
+                                   blsk::FEXP_PARK_WORDS(want)) * 4));  // LN doubles as the final exp's park
   static_assert(3 * blsk::F_WORDS >= 48 * 64 / 21 + 1, "FW holds the Miller park of a sub-chunk");
   HIPCHK(c, c->h_inf.ensure(want));
   HIPCHK(c, c->s_inf.ensure(want));
@@ -257,7 +257,7 @@ static int run_tail(blsv_ctx* c, const uint8_t* d_sigs, size_t stride, size_t of
   }
   {
     StageTimer tm(c, ST_FEXP, cnt, st);
-    // the 3-lane products park in LN (free after the Miller stage)
+    // the final exponentiation parks its kept squares and 3-lane products in LN (free after the Miller stage)
     blsk::launch_final_exp(c->F.as<uint32_t>(), c->FW.as<uint32_t>(), cnt, c->cls.as<uint8_t>(), st,
                            c->LN.as<uint32_t>());
   }

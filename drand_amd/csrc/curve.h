@@ -149,16 +149,30 @@ DI bool jac_eq(const jac<F>& p, const jac<F>& q) {
 // G2 doubling (dbl-2009-l, as jac_dbl) with the Fp2 products expanded in place: the [x] chains of
 // the G2 cofactor clearing and subgroup check run their 63 doublings call-free, so the register
 // allocator sees the whole step instead of the AMDGPU call ABI's caller/callee-saved split.
+#ifndef BLS_G2_DBL_FENCE
+#define BLS_G2_DBL_FENCE 0
+#endif
+#if BLS_G2_DBL_FENCE
+#define G2_DBL_FENCE() BLS_SCHED_FENCE()
+#else
+#define G2_DBL_FENCE() ((void)0)
+#endif
 DI g2j g2_dbl_inl(const g2j& p) {
+  const fp2 Z3 = fp2_dbl(fp2_mul_inl(p.y, p.z));
+  G2_DBL_FENCE();
   const fp2 A = fp2_sqr_inl(p.x);
+  G2_DBL_FENCE();
   const fp2 B = fp2_sqr_inl(p.y);
+  G2_DBL_FENCE();
   const fp2 C = fp2_sqr_inl(B);
+  G2_DBL_FENCE();
   const fp2 D = fp2_dbl(fp2_sub(fp2_sub(fp2_sqr_inl(fp2_add(p.x, B)), A), C));
+  G2_DBL_FENCE();
   const fp2 E = fp2_add(fp2_dbl(A), A);
   const fp2 X3 = fp2_sub(fp2_sqr_inl(E), fp2_dbl(D));
+  G2_DBL_FENCE();
   const fp2 C8 = fp2_dbl(fp2_dbl(fp2_dbl(C)));
   const fp2 Y3 = fp2_sub(fp2_mul_inl(E, fp2_sub(D, X3)), C8);
-  const fp2 Z3 = fp2_dbl(fp2_mul_inl(p.y, p.z));
   return {X3, Y3, Z3};
 }
 
@@ -222,6 +236,97 @@ DI bool g2_in_subgroup(const g2j& p) {
   if (jac_is_inf(p)) return true;
   g2j xp = jac_neg(jac_mul_x_abs(p));
   return jac_eq(g2_psi(p), xp);
+}
+
+// ------------------------------------------------------------ call-free [x] chains (2 waves/SIMD)
+// A called Fp2 product makes everything live across it sit in the ~112 callee-saved VGPRs; the
+// chain's point, its base point and a step's temporaries do not fit, so a called addition spills
+// (7 KB/lane at 2 waves/SIMD for the subgroup check) and the chains ran at 1 wave/SIMD. Here the
+// additions are expanded in place too, with the base point re-read from staging at each of its 5
+// uses; only the exceptional cases (P == +-Q, a point at infinity) take a rarely executed branch
+// through the called formulas. Same results as jac_add / jac_add_aff.
+// add-2007-bl (as jac_add)
+DI g2j g2_add_inl(const g2j& p, const g2j& q) {
+  const fp2 Z1Z1 = fp2_sqr_inl(p.z);
+  const fp2 Z2Z2 = fp2_sqr_inl(q.z);
+  const fp2 U1 = fp2_mul_inl(p.x, Z2Z2);
+  const fp2 U2 = fp2_mul_inl(q.x, Z1Z1);
+  const fp2 S1 = fp2_mul_inl(fp2_mul_inl(p.y, q.z), Z2Z2);
+  const fp2 S2 = fp2_mul_inl(fp2_mul_inl(q.y, p.z), Z1Z1);
+  const fp2 H = fp2_sub(U2, U1);
+  const fp2 r = fp2_dbl(fp2_sub(S2, S1));
+  const fp2 I = fp2_sqr_inl(fp2_dbl(H));
+  const fp2 J = fp2_mul_inl(H, I);
+  const fp2 V = fp2_mul_inl(U1, I);
+  const fp2 X3 = fp2_sub(fp2_sub(fp2_sqr_inl(r), J), fp2_dbl(V));
+  const fp2 Y3 = fp2_sub(fp2_mul_inl(r, fp2_sub(V, X3)), fp2_dbl(fp2_mul_inl(S1, J)));
+  const fp2 Z3 = fp2_mul_inl(fp2_sub(fp2_sub(fp2_sqr_inl(fp2_add(p.z, q.z)), Z1Z1), Z2Z2), H);
+  g2j out = {X3, Y3, Z3};
+  const bool pinf = jac_is_inf(p), qinf = jac_is_inf(q), h0 = fp2_is_zero(H);
+  if (pinf | qinf | h0) {  // per lane, rare
+    const bool r0 = fp2_is_zero(r);
+    out = pinf ? q : (qinf ? p : (r0 ? jac_dbl(p) : jac_infinity<fp2>()));
+  }
+  return out;
+}
+
+// madd-2007-bl (as jac_add_aff), q affine and never infinity
+DI g2j g2_madd_inl(const g2j& p, const g2a& q) {
+  const fp2 Z1Z1 = fp2_sqr_inl(p.z);
+  const fp2 U2 = fp2_mul_inl(q.x, Z1Z1);
+  const fp2 S2 = fp2_mul_inl(fp2_mul_inl(q.y, p.z), Z1Z1);
+  const fp2 H = fp2_sub(U2, p.x);
+  const fp2 r = fp2_dbl(fp2_sub(S2, p.y));
+  const fp2 HH = fp2_sqr_inl(H);
+  const fp2 I = fp2_dbl(fp2_dbl(HH));
+  const fp2 J = fp2_mul_inl(H, I);
+  const fp2 V = fp2_mul_inl(p.x, I);
+  const fp2 X3 = fp2_sub(fp2_sub(fp2_sqr_inl(r), J), fp2_dbl(V));
+  const fp2 Y3 = fp2_sub(fp2_mul_inl(r, fp2_sub(V, X3)), fp2_dbl(fp2_mul_inl(p.y, J)));
+  const fp2 Z3 = fp2_sub(fp2_sub(fp2_sqr_inl(fp2_add(p.z, H)), Z1Z1), HH);
+  g2j out = {X3, Y3, Z3};
+  const bool pinf = jac_is_inf(p), h0 = fp2_is_zero(H);
+  if (pinf | h0) {
+    const bool r0 = fp2_is_zero(r);
+    out = pinf ? jac_from_aff(q) : (r0 ? jac_dbl(p) : jac_infinity<fp2>());
+  }
+  return out;
+}
+
+// [|x|] P call-free; base() returns P again at each addition (affine for AFF: mixed additions)
+template <bool AFF, typename Base>
+DI g2j g2_mul_x_abs_inl(const g2j& p, Base base) {
+  g2j acc = p;
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    acc = g2_dbl_inl(acc);
+    if ((BLS_X_ABS >> i) & 1ull) {
+      if constexpr (AFF)
+        acc = g2_madd_inl(acc, base());
+      else
+        acc = g2_add_inl(acc, base());
+    }
+  }
+  return acc;
+}
+
+// g2_in_subgroup for an affine point re-read by `reload` (never infinity: the caller screens it)
+template <typename Reload>
+DI bool g2_in_subgroup_aff_reload(Reload reload) {
+  const g2j xp = jac_neg(g2_mul_x_abs_inl<true>(jac_from_aff(reload()), reload));
+  return jac_eq(g2_psi(jac_from_aff(reload())), xp);
+}
+
+// g2_clear_cofactor_reload with call-free chains: stash(A) parks A = [x]P + psi(P) (the second
+// chain's base) and reload_a() re-reads it
+template <typename Reload, typename Stash, typename ReloadA>
+DI g2j g2_clear_cofactor_inl(Reload reload, Stash stash, ReloadA reload_a) {
+  g2j a = jac_add(jac_neg(g2_mul_x_abs_inl<false>(reload(), reload)), g2_psi(reload()));
+  stash(a);
+  g2j r = jac_add(jac_neg(g2_mul_x_abs_inl<false>(a, reload_a)), jac_neg(reload_a()));
+  const g2j p = reload();
+  r = jac_add(r, jac_neg(p));
+  return jac_add(r, g2_psi2(jac_dbl(p)));
 }
 
 // RFC 9380 G.3 clear_cofactor_bls12381_g2: h_eff P = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)
@@ -294,7 +399,8 @@ DI uint8_t g2_decompress(const uint8_t* in, g2a& out, bool& is_inf, bool check_s
   if (fp2_lex_largest(y) != sign) y = fp2_neg(y);
   out.x = x;
   out.y = y;
-  if (check_subgroup && !g2_in_subgroup(jac_from_aff(out))) return REJ_NOT_IN_SUBGROUP;
+  // the device chain (k_subgroup_g2: mixed additions with the affine point)
+  if (check_subgroup && !g2_in_subgroup_aff_reload([&]() { return out; })) return REJ_NOT_IN_SUBGROUP;
   return REJ_OK;
 }
 

@@ -263,4 +263,130 @@ DI fp12 final_exponentiation(const fp12& f) {
   return fexp_step<4>([&]() { return t; }, [&]() { return c; }, [&]() { return g; });
 }
 
+// ---------------------------------------------------------------- compressed cyclotomic squaring
+// Karabina (eprint 2010/542) for X in the cyclotomic subgroup, in the w-power basis f = sum c_k w^k:
+// the squaring of (c1, c2, c4, c5) never needs c0 or c3. With A1 = c1 + c4 s, A2 = c2 + c5 s
+// (Fp4 = Fp2[s], s = w^3, s^2 = xi) and Y_j = A_j^2:
+//   c1' = 2 c1 + 3 xi Y2.b   c4' = 3 Y2.a - 2 c4   c2' = 3 Y1.a - 2 c2   c5' = 2 c5 + 3 Y1.b
+// i.e. the Granger-Scott square restricted to the thirds A1, A2 (tri.h roles 1 and 2): 6 Fp2 squares
+// instead of 9. Decompression recovers the dropped coefficients (identities checked against the
+// oracle's Fp12 arithmetic on random cyclotomic elements, tests/test_abi.py):
+//   c3 = (xi c5^2 + 3 c2^2 - 2 c4) / (4 c1)       (c1 != 0)
+//   c3 = 2 c2 c5 / c4                            (c1 == 0: c3 c4 - 2 c2 c5 = c1 (1 - i)(1 - c0) / 2)
+//   c0 = xi (2 c3^2 + c1 c5 - 3 c4 c2) + 1
+// and c1 = c4 = 0 only for X = 1 (numerator 0 over denominator 1 then gives c3 = 0, c0 = 1).
+// X^|x| = prod_b X^(2^b) over the set bits b = 16, 48, 57, 60, 62, 63 of |x|: 63 compressed squares,
+// six decompressions sharing one Fp2 inversion (Montgomery's trick), 5 multiplications.
+struct fp12c {
+  fp2 c1, c4, c2, c5;  // A1 = (c1, c4), A2 = (c2, c5)
+};
+
+DI fp12c fp12_compress(const fp12& x) { return {x.c1.c0, x.c0.c2, x.c0.c1, x.c1.c2}; }
+
+// (a + b s)^2 = (a^2 + xi b^2) + 2ab s as (square part, cross part): 3 Fp2 squares. INL: the squares
+// expanded in place, one after the other (call-free squaring kernels, k_fexp.hip)
+template <bool INL = false>
+DI void fp4_sqr_parts(const fp2& a, const fp2& b, fp2& sq, fp2& cross) {
+  auto sqr = [](const fp2& v) { return INL ? fp2_sqr_inl(v) : fp2_sqr(v); };
+  const fp2 t0 = sqr(a);
+  BLS_SCHED_FENCE();
+  const fp2 t1 = sqr(b);
+  BLS_SCHED_FENCE();
+  const fp2 t2 = sqr(fp2_add_lazy(a, b));
+  BLS_SCHED_FENCE();
+  sq = fp2_add(t0, fp2_mul_xi(t1));
+  cross = fp2_sub(t2, fp2_add(t0, t1));
+}
+
+template <bool INL = false>
+DI fp12c karabina_sqr(const fp12c& x) {
+  fp2 y1a, y1b, y2a, y2b;
+  fp4_sqr_parts<INL>(x.c1, x.c4, y1a, y1b);
+  fp4_sqr_parts<INL>(x.c2, x.c5, y2a, y2b);
+  return {fp2_add(fp2_dbl(x.c1), fp2_mul3(fp2_mul_xi(y2b))), fp2_sub(fp2_mul3(y2a), fp2_dbl(x.c4)),
+          fp2_sub(fp2_mul3(y1a), fp2_dbl(x.c2)), fp2_add(fp2_dbl(x.c5), fp2_mul3(y1b))};
+}
+
+// The third A0 = c0 + c3 s evolves on its own under the cyclotomic square (tower.h
+// fp12_cyclotomic_sqr: z0, z1 depend only on A0^2): (c0, c3) <- (3 Y.a - 2 c0, 3 Y.b + 2 c3), Y = A0^2.
+// With karabina_sqr this is the whole Granger-Scott square, split into two independent chains.
+template <bool INL = false>
+DI void cyclotomic_sqr_a0(fp2& c0, fp2& c3) {
+  fp2 ya, yb;
+  fp4_sqr_parts<INL>(c0, c3, ya, yb);
+  c0 = fp2_sub(fp2_mul3(ya), fp2_dbl(c0));
+  c3 = fp2_add(fp2_mul3(yb), fp2_dbl(c3));
+}
+
+// numerator / denominator of c3 (branch-free selection of the three cases above)
+DI void karabina_num_den(const fp12c& x, fp2& num, fp2& den) {
+  const bool z1 = fp2_is_zero(x.c1), z4 = fp2_is_zero(x.c4);
+  const fp2 n_main = fp2_sub(fp2_add(fp2_mul_xi(fp2_sqr(x.c5)), fp2_mul3(fp2_sqr(x.c2))), fp2_dbl(x.c4));
+  const fp2 n_alt = fp2_dbl(fp2_mul(x.c2, x.c5));
+  num = fp2_select(z1, fp2_select(z4, fp2_zero(), n_alt), n_main);
+  den = fp2_select(z1, fp2_select(z4, fp2_one(), x.c4), fp2_dbl(fp2_dbl(x.c1)));
+}
+
+// c0 from the other five coefficients
+DI fp2 karabina_c0(const fp12c& x, const fp2& c3) {
+  const fp2 t = fp2_sub(fp2_add(fp2_dbl(fp2_sqr(c3)), fp2_mul(x.c1, x.c5)), fp2_mul3(fp2_mul(x.c4, x.c2)));
+  return fp2_add(fp2_mul_xi(t), fp2_one());
+}
+
+DI fp12 fp12_from_compressed(const fp12c& x, const fp2& c0, const fp2& c3) { return {{c0, x.c2, x.c4}, {x.c1, c3, x.c5}}; }
+
+constexpr int KARABINA_N = 6;  // set bits of |x|
+// squaring count after which X^(2^b) is kept, b = 16, 48, 57, 60, 62, 63 (one bit each of KARABINA_KEEP)
+constexpr uint64_t KARABINA_KEEP = BLS_X_ABS;
+
+// X^|x| in registers (host op counter, test hook): the device runs the same three phases as kernels
+// (k_fexp.hip: duo squaring chain, one-lane batch decompression, 3-lane products)
+DI fp12 fp12_pow_x_abs_karabina(const fp12& X) {
+  fp12c c = fp12_compress(X);
+  fp12c S[KARABINA_N];
+  int e = 0;
+  for (int k = 1; k <= 63; k++) {
+    c = karabina_sqr(c);
+    if ((KARABINA_KEEP >> k) & 1ull) S[e++] = c;
+  }
+  fp2 num[KARABINA_N], den[KARABINA_N], pre[KARABINA_N];
+  for (int j = 0; j < KARABINA_N; j++) {
+    karabina_num_den(S[j], num[j], den[j]);
+    pre[j] = j ? fp2_mul(pre[j - 1], den[j]) : den[j];
+  }
+  fp2 inv = fp2_inv(pre[KARABINA_N - 1]);
+  fp12 r = fp12_one();
+  for (int j = KARABINA_N - 1; j >= 0; j--) {
+    const fp2 dinv = j ? fp2_mul(inv, pre[j - 1]) : inv;
+    if (j) inv = fp2_mul(inv, den[j]);
+    const fp2 c3 = fp2_mul(num[j], dinv);
+    const fp12 D = fp12_from_compressed(S[j], karabina_c0(S[j], c3), c3);
+    r = j == KARABINA_N - 1 ? D : fp12_mul(r, D);
+  }
+  return r;
+}
+
+// fexp_step<MODE> with X^|x| from the compressed chain
+template <int MODE, typename LX, typename LC, typename LG>
+DI fp12 fexp_step_karabina(LX lx, LC lc, LG lg) {
+  fp12 r = fp12_conj(fp12_pow_x_abs_karabina(lx()));
+  if (MODE == 0 || MODE == 1) return fp12_mul(r, fp12_conj(lx()));
+  if (MODE == 2) return fp12_mul(r, fp12_frob(lx()));
+  if (MODE == 3) return r;
+  r = fp12_mul(r, fp12_frob2(lc()));
+  r = fp12_mul(r, fp12_conj(lc()));
+  r = fp12_mul(r, fp12_cyclotomic_sqr(lg()));
+  return fp12_mul(r, lg());
+}
+
+DI fp12 final_exponentiation_karabina(const fp12& f) {
+  const fp12 g = fexp_easy(f);
+  auto none = [&]() { return g; };
+  const fp12 a = fexp_step_karabina<0>([&]() { return g; }, none, none);
+  const fp12 b = fexp_step_karabina<1>([&]() { return a; }, none, none);
+  const fp12 c = fexp_step_karabina<2>([&]() { return b; }, none, none);
+  const fp12 t = fexp_step_karabina<3>([&]() { return c; }, none, none);
+  return fexp_step_karabina<4>([&]() { return t; }, [&]() { return c; }, [&]() { return g; });
+}
+
 }  // namespace bls

@@ -368,6 +368,37 @@ DI fp4 tri_frob2(const tri_lane& t, const fp4& x) {
   return {fp2_mul_fp(x.a, ga), fp2_mul_fp(x.b, gb)};
 }
 
+// ------------------------------------------------------------------ two lanes per Fp12 ("duo")
+// The compressed cyclotomic square (pairing.h karabina_sqr) touches only the thirds A1 = (c1, c4) and
+// A2 = (c2, c5): lane pair (2j, 2j + 1) holds A1 (role 1, even lane) and A2 (role 2) of beacon j, 32
+// beacons per wave and no idle lane. The partner's square crosses over DPP quad_perm [1, 0, 3, 2]
+// (one VALU move per word, no LDS round trip).
+constexpr int DUO_GROUPS = 32;
+DI fp duo_swap(const fp& v) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.l[i], 0xB1, 0xf, 0xf, false);
+  return r;
+}
+DI fp2 duo_swap2(const fp2& v) { return {duo_swap(v.c0), duo_swap(v.c1)}; }
+
+// tri_cyclotomic_sqr for roles 1 and 2 only (role 1: r1 = true), call-free:
+//   role 1: (c1, c4) <- (2 c1 + 3 xi Y2.b, 3 Y2.a - 2 c4)   role 2: (c2, c5) <- (3 Y1.a - 2 c2, 2 c5 + 3 Y1.b)
+DI fp4 duo_karabina_sqr(bool r1, const fp4& x) {
+  // the three squares one after the other (fenced): interleaved, they would double the live set
+  const fp2 t0 = fp2_sqr_inl(x.a);
+  BLS_SCHED_FENCE();
+  const fp2 t1 = fp2_sqr_inl(x.b);
+  BLS_SCHED_FENCE();
+  const fp2 t2 = fp2_sqr_inl(fp2_add_lazy(x.a, x.b));
+  BLS_SCHED_FENCE();
+  const fp4 sq = {fp2_add(t0, fp2_mul_xi(t1)), fp2_sub(fp2_sub(t2, t0), t1)};
+  const fp2 ya = duo_swap2(sq.a), yb = duo_swap2(sq.b);
+  const fp2 u3 = fp2_mul3(fp2_select(r1, fp2_mul_xi(yb), ya)), v3 = fp2_mul3(fp2_select(r1, ya, yb));
+  const fp2 a2 = fp2_dbl(x.a), b2 = fp2_dbl(x.b);
+  return {fp2_select(r1, fp2_add(u3, a2), fp2_sub(u3, a2)), fp2_select(r1, fp2_sub(v3, b2), fp2_add(v3, b2))};
+}
+
 // this lane's part of "f == 1": role 0 must hold (1, 0), roles 1, 2 zero; combined over the group
 DI bool tri_is_one(const tri_lane& t, const fp4& x) {
   const fp2 want_a = fp2_select(t.role == 0, fp2_one(), fp2_zero());

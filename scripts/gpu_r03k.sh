@@ -1,0 +1,15 @@
+# call-free G2 [x] chains at 2 waves/SIMD (subgroup check, cofactor clearing): full GPU suite, then
+# same-box A/B against the 1-wave called chains (variants/g2old) and the split-accumulator multiplier
+# in the final exponentiation / hash units (variants/fexpilp, hashilp); serial-stage kernel stats
+set -o pipefail
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r03k
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit 12
+for v in main g2old fexpilp hashilp main; do
+  lib=$PWD/drand_amd/libblsverify.so; [ $v = main ] || lib=$PWD/variants/libblsverify_$v.so
+  DRAND_AMD_LIB=$lib timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --cpu-per-worker 0 >> $O/bench_$v.json 2>> $O/bench_$v.err || exit 13
+done
+BLSV_SERIAL_STAGES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --cpu-per-worker 0 > $O/bench_serial_prof.json 2> $O/prof.log || exit 16
+echo done
