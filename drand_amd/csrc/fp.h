@@ -450,6 +450,14 @@ DI fp fp_from_u12(const u12& v) {
 }
 
 DI fp fp_mul(const fp& a, const fp& b) { return fp_from_u12(fp_mul_u12(fp_to_u12(a), fp_to_u12(b))); }
+// fp_mul expanded in place (same column sums, same result) for call-free loops
+DI fp fp_mul_inl(const fp& a, const fp& b) {
+  BLS_COUNT_MUL();
+  uint32_t x[14], y[14];
+  fp_split28(fp_to_u12(a), x);
+  fp_split28(fp_to_u12(b), y);
+  return fp_from_u12(fp_mont_dot<false>(x, y, x, y));
+}
 
 DI fp fp_sqr(const fp& a) { return fp_from_u12(fp_sqr_u12(fp_to_u12(a))); }
 

@@ -41,6 +41,40 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
       st_fp2(LN, sub, i, s + 2, o.a1);
       st_fp2(LN, sub, i, s + 4, o.a4);
     };
+#if BLS_LINES_INL == 2
+    // call-free steps (pairing.h miller_dbl_step_inl): P, Q and the lines never live across a call
+    auto pcoord = [&](int c) {
+      size_t o = (size_t)kk * G1_WORDS + 12 * c;
+      asm volatile("" : "+v"(o));  // re-read at the use
+      fp v;
+#pragma unroll
+      for (int w = 0; w < 12; w++) v.l[w] = pk_tab[o + w];
+      return k == 0 ? v : fp_load_const(c == 0 ? G1_GEN_X : G1_GEN_NEG_Y);
+    };
+    if (!act[k]) {  // a skipped pair (a point at infinity) contributes the line 1 at every step
+#pragma unroll 1
+      for (int s = 0; s < MILLER_STEPS; s++) emit(s, line_one());
+      return;
+    }
+    int step = 0;
+    auto put = [&](int c, const fp2& v) { st_fp2(LN, sub, i, line_slot(step, k) + 2 * c, v); };
+    auto xp = [&]() { return pcoord(0); };
+    auto yp = [&]() { return pcoord(1); };
+    g2proj T;
+    {
+      const g2a Q0 = load_q();
+      T = {Q0.x, Q0.y, fp2_one()};
+    }
+#pragma unroll 1
+    for (int b = 62; b >= 0; b--) {
+      miller_dbl_step_inl(T, put, xp, yp);
+      step++;
+      if ((BLS_X_ABS >> b) & 1ull) {
+        miller_add_step_inl(T, load_q, put, xp, yp);
+        step++;
+      }
+    }
+#else
     g1a P;
     if (k == 0) {
 #pragma unroll
@@ -53,6 +87,7 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
       P.y = fp_load_const(G1_GEN_NEG_Y);
     }
     miller_lines(P, load_q, emit);
+#endif
   }
 }
 

@@ -50,8 +50,79 @@ DI void miller_dbl_step(g2proj& t, fp2& l00, fp2& l01, fp2& l11, const fp& xp, c
 }
 
 #ifndef BLS_LINES_INL
-#define BLS_LINES_INL 0
+#define BLS_LINES_INL 2
 #endif
+
+// Call-free Miller steps (k_miller_lines at 2 waves/SIMD, BLS_LINES_INL == 2): every product expanded
+// in place, one after the other (fenced), ordered so that few values are live at once, and each
+// line coefficient handed to put(c, v) (c = 0: l00, 1: l01, 2: l11) as soon as it is known; xp()/yp()
+// and the addition's q() re-read their operands at the use. Same operations on the same values as
+// miller_dbl_step / miller_add_step, so the lines are bit-identical.
+template <typename Put, typename XP, typename YP>
+DI void miller_dbl_step_inl(g2proj& t, Put put, XP xp, YP yp) {
+  const fp2 B = fp2_sqr_inl(t.y);
+  BLS_SCHED_FENCE();
+  const fp2 C = fp2_sqr_inl(t.z);
+  BLS_SCHED_FENCE();
+  const fp2 H = fp2_sub(fp2_sqr_inl(fp2_add_lazy(t.y, t.z)), fp2_add(B, C));
+  BLS_SCHED_FENCE();
+  put(2, fp2_neg(fp2_mul_fp_inl(H, yp())));
+  BLS_SCHED_FENCE();
+  const fp2 Z3 = fp2_mul_inl(B, H);
+  BLS_SCHED_FENCE();
+  const fp2 E = fp2_mul_3b(C);
+  const fp2 F = fp2_mul3(E);
+  const fp2 G = fp2_half(fp2_add(B, F));
+  put(0, fp2_sub(E, B));
+  const fp2 BF = fp2_sub(B, F);
+  const fp2 A = fp2_half(fp2_mul_inl(t.x, t.y));
+  BLS_SCHED_FENCE();
+  const fp2 X3 = fp2_mul_inl(A, BF);
+  BLS_SCHED_FENCE();
+  put(1, fp2_mul_fp_inl(fp2_mul3(fp2_sqr_inl(t.x)), xp()));
+  BLS_SCHED_FENCE();
+  const fp2 G2 = fp2_sqr_inl(G);
+  BLS_SCHED_FENCE();
+  const fp2 Y3 = fp2_sub(G2, fp2_mul3(fp2_sqr_inl(E)));
+  t = {X3, Y3, Z3};
+}
+
+template <typename Put, typename Q, typename XP, typename YP>
+DI void miller_add_step_inl(g2proj& t, Q qload, Put put, XP xp, YP yp) {
+  fp2 theta, delta;
+  {
+    const g2a q = qload();
+    theta = fp2_sub(t.y, fp2_mul_inl(q.y, t.z));
+    BLS_SCHED_FENCE();
+    delta = fp2_sub(t.x, fp2_mul_inl(q.x, t.z));
+    BLS_SCHED_FENCE();
+    const fp2 u = fp2_mul_inl(theta, q.x);
+    BLS_SCHED_FENCE();
+    put(0, fp2_sub(u, fp2_mul_inl(delta, q.y)));
+    BLS_SCHED_FENCE();
+  }
+  put(1, fp2_neg(fp2_mul_fp_inl(theta, xp())));
+  BLS_SCHED_FENCE();
+  put(2, fp2_mul_fp_inl(delta, yp()));
+  BLS_SCHED_FENCE();
+  const fp2 C = fp2_sqr_inl(theta);
+  BLS_SCHED_FENCE();
+  const fp2 D = fp2_sqr_inl(delta);
+  BLS_SCHED_FENCE();
+  const fp2 E = fp2_mul_inl(D, delta);
+  BLS_SCHED_FENCE();
+  const fp2 F = fp2_mul_inl(t.z, C);
+  BLS_SCHED_FENCE();
+  const fp2 G = fp2_mul_inl(t.x, D);
+  BLS_SCHED_FENCE();
+  const fp2 H = fp2_sub(fp2_add(E, F), fp2_dbl(G));
+  const fp2 X3 = fp2_mul_inl(delta, H);
+  BLS_SCHED_FENCE();
+  const fp2 Y3 = fp2_sub(fp2_mul_inl(theta, fp2_sub(G, H)), fp2_mul_inl(t.y, E));
+  BLS_SCHED_FENCE();
+  const fp2 Z3 = fp2_mul_inl(t.z, E);
+  t = {X3, Y3, Z3};
+}
 
 DI void miller_add_step(g2proj& t, const g2a& q, fp2& l00, fp2& l01, fp2& l11, const fp& xp, const fp& yp) {
   fp2 theta = fp2_sub(t.y, fp2_mul(q.y, t.z));
@@ -152,7 +223,7 @@ DI void miller_lines(const g1a& P, LoadQ load_q, Emit emit) {
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
     line l;
-    miller_dbl_step<BLS_LINES_INL != 0>(T, l.a0, l.a1, l.a4, P.x, P.y);
+    miller_dbl_step<BLS_LINES_INL == 1>(T, l.a0, l.a1, l.a4, P.x, P.y);
     emit(step++, l);
     if ((BLS_X_ABS >> i) & 1ull) {
       miller_add_step(T, load_q(), l.a0, l.a1, l.a4, P.x, P.y);

@@ -58,6 +58,11 @@ DI fp2 fp2_sqr_inl(const fp2& a) {
 }
 
 DI fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
+DI fp2 fp2_mul_fp_inl(const fp2& a, const fp& b) {
+  const fp c0 = fp_mul_inl(a.c0, b);
+  BLS_SCHED_FENCE();
+  return {c0, fp_mul_inl(a.c1, b)};
+}
 DI fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1)}; }
 
 // multiply by xi = 1 + i: (a0 - a1) + (a0 + a1) i
