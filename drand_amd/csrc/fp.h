@@ -155,6 +155,28 @@ DI fp fp_sub(const fp& a, const fp& b) {
   return r;
 }
 
+// sub ? a - b : a + b for a, b in [0, 2p), result in [0, 2p): one operation whose direction is data
+// (the 3-lane kernels pick it per lane role) instead of both results and a select.
+//   chain 1: s = a + (b ^ m) + sub          (m = all ones when sub: a + ~b + 1 = a - b + 2^384)
+//   chain 2: d = s + (2p ^ k) + !sub        (k = all ones when adding: d = s - 2p;  else d = s + 2p)
+// adding: d is right iff s >= 2p (chain 2 carries out); subtracting: d is right iff a < b (chain 1
+// does not carry out)
+DI fp fp_addsub(const fp& a, const fp& b, bool sub) {
+  const uint32_t m = sub ? 0xffffffffu : 0u;
+  uint32_t s[12], d[12];
+  unsigned c1 = sub ? 1u : 0u;
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = __builtin_addc(a.l[i], b.l[i] ^ m, c1, &c1);
+  unsigned c2 = sub ? 0u : 1u;
+#pragma unroll
+  for (int i = 0; i < 12; i++) d[i] = __builtin_addc(s[i], P2_RAW[i] ^ ~m, c2, &c2);
+  const bool take_d = sub ? (c1 == 0u) : (c2 != 0u);
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = take_d ? d[i] : s[i];
+  return r;
+}
+
 // 2p - a, or 0 for a == 0 (keeps the result below 2p)
 DI fp fp_neg(const fp& a) {
   uint32_t d[12];

@@ -31,6 +31,7 @@ DI fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(
 // operand contract)
 DI fp2 fp2_add_lazy(const fp2& a, const fp2& b) { return {fp_add_lazy(a.c0, b.c0), fp_add_lazy(a.c1, b.c1)}; }
 DI fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+DI fp2 fp2_addsub(const fp2& a, const fp2& b, bool sub) { return {fp_addsub(a.c0, b.c0, sub), fp_addsub(a.c1, b.c1, sub)}; }
 DI fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
 DI fp2 fp2_neg(const fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
 DI fp2 fp2_conj(const fp2& a) { return {a.c0, fp_neg(a.c1)}; }

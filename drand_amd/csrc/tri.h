@@ -23,6 +23,11 @@ namespace bls {
 
 constexpr int TRI_GROUPS = 21;  // beacons per 64-lane wave
 
+// role-dependent additions as one fp_addsub (direction as data) instead of both results + a select
+#ifndef BLS_TRI_ADDSUB
+#define BLS_TRI_ADDSUB 1
+#endif
+
 struct fp4 {
   fp2 a, b;  // a + b s
 };
@@ -31,6 +36,7 @@ DI fp4 fp4_add(const fp4& x, const fp4& y) { return {fp2_add(x.a, y.a), fp2_add(
 DI fp4 fp4_sub(const fp4& x, const fp4& y) { return {fp2_sub(x.a, y.a), fp2_sub(x.b, y.b)}; }
 DI fp4 fp4_dbl(const fp4& x) { return {fp2_dbl(x.a), fp2_dbl(x.b)}; }
 DI fp4 fp4_add_lazy(const fp4& x, const fp4& y) { return {fp2_add_lazy(x.a, y.a), fp2_add_lazy(x.b, y.b)}; }
+DI fp4 fp4_addsub(const fp4& x, const fp4& y, bool sub) { return {fp2_addsub(x.a, y.a, sub), fp2_addsub(x.b, y.b, sub)}; }
 DI fp4 fp4_select(bool c, const fp4& x, const fp4& y) { return {fp2_select(c, x.a, y.a), fp2_select(c, x.b, y.b)}; }
 // x * s = xi b + a s
 DI fp4 fp4_mul_s(const fp4& x) { return {fp2_mul_xi(x.b), x.a}; }
@@ -120,9 +126,15 @@ DI fp4 tri_cyclotomic_sqr(const tri_lane& t, const fp4& x) {
   const bool r1 = t.role == 1;
   const fp2 u = fp2_select(r1, fp2_mul_xi(y.b), y.a);
   const fp2 v = fp2_select(r1, y.a, y.b);
+#if BLS_TRI_ADDSUB
+  // 3u +- 2a = 2(u +- a) + u: one direction-by-role addition instead of both and a select
+  const fp2 ta = fp2_addsub(u, x.a, !r1), tb = fp2_addsub(v, x.b, r1);
+  return {fp2_add(fp2_dbl(ta), u), fp2_add(fp2_dbl(tb), v)};
+#else
   const fp2 u3 = fp2_add(fp2_dbl(u), u), v3 = fp2_add(fp2_dbl(v), v);
   const fp2 a2 = fp2_dbl(x.a), b2 = fp2_dbl(x.b);
   return {fp2_select(r1, fp2_add(u3, a2), fp2_sub(u3, a2)), fp2_select(r1, fp2_sub(v3, b2), fp2_add(v3, b2))};
+#endif
 }
 
 // general product (Karatsuba over the cubic): lane j forms P_j = A_j B_j and
@@ -328,12 +340,20 @@ DI fp4 tri_mul_lp(const tri_lane& t, const fp4& a, const fp4& b, uint32_t* park,
   {
     const fp4 Pn = xchg_fp4(P, t.next_b);
     const fp4 u = fp4_select(t.role == 2, Pn, fp4_mul_s(Pn));
+#if BLS_TRI_ADDSUB
+    R = fp4_addsub(R, u, t.role != 1);
+#else
     R = fp4_add(R, fp4_select(t.role == 1, u, fp4_neg(u)));
+#endif
   }
   {
     const fp4 Pp = xchg_fp4(P, t.prev_b);
     const fp4 u = fp4_select(t.role == 0, fp4_mul_s(Pp), Pp);
+#if BLS_TRI_ADDSUB
+    R = fp4_addsub(R, u, t.role != 2);
+#else
     R = fp4_add(R, fp4_select(t.role == 2, u, fp4_neg(u)));
+#endif
   }
   {
     size_t j = park_i;
