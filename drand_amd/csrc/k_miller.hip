@@ -169,6 +169,11 @@ BLS_KERNEL(BLS_WPE_MILLER_F) k_miller_f(const uint32_t* LN, const uint8_t* cls, 
       if (rep == 0 && b != 62) f = fp12_sqr(f);
       {
         const fp12 L = line_mul_line(load(step, 0), load(step, 1));
+        if (step == 0) {  // f = 1 * L: the first line pair is f itself
+          f = L;
+          step++;
+          continue;
+        }
         mf_put(0, L.c0.c0);
         mf_put(1, L.c0.c1);
         mf_put(2, L.c0.c2);

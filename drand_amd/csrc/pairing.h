@@ -192,7 +192,8 @@ DI fp12 miller_loop_2(const g1a (&P)[2], const g2a (&Q)[2], const bool (&active)
       miller_dbl_step(T[k], l[k].a0, l[k].a1, l[k].a4, P[k].x, P[k].y);
       if (!active[k]) l[k] = line_one();
     }
-    f = fp12_mul_by_line_pair(f, line_mul_line(l[0], l[1]));
+    // f = 1 at the first step: the line pair is f itself
+    f = first ? line_mul_line(l[0], l[1]) : fp12_mul_by_line_pair(f, line_mul_line(l[0], l[1]));
     first = false;
     if ((BLS_X_ABS >> i) & 1ull) {
 #pragma unroll
@@ -240,7 +241,8 @@ DI fp12 miller_f_from_lines(LoadLine load) {
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
     if (i != 62) f = fp12_sqr(f);
-    f = fp12_mul_by_line_pair(f, line_mul_line(load(step, 0), load(step, 1)));
+    const fp12 L = line_mul_line(load(step, 0), load(step, 1));
+    f = step == 0 ? L : fp12_mul_by_line_pair(f, L);
     step++;
     if ((BLS_X_ABS >> i) & 1ull) {
       f = fp12_mul_by_line_pair(f, line_mul_line(load(step, 0), load(step, 1)));
