@@ -417,10 +417,16 @@ DI u24 fp2_mul_body(const u24& a, const u12& b0, const u12& b1) {
   return u24_of(c0, c1);
 }
 
-// Fp2 square: c0 = (a0 + a1)(a0 + 4p - a1), c1 = (2 a0) a1. A squaring operand is at most ONE lazy
-// sum (< 4p; every fp2_sqr* call site squares a reduced value or one fp2_add_lazy), so the 12-word
-// sums stay below 8p < 2^384 (a smaller live set than radix-2^28 sums: the inlined cyclotomic squares
-// of the 3-lane final exponentiation are register-bound).
+// Fp2 square: c0 = (a0 + a1)(a0 + 16p - a1), c1 = (2 a0) a1, the sums formed limb-wise in radix 2^28
+// after splitting a0 and a1 once (no carry chains: a0 + a1 has limbs < 2^29, a0 + 16p - a1 < 2^29.6
+// against NEG28_16P, whose limbs are at least any operand limb). A squaring operand is at most ONE
+// lazy sum (< 4p; every fp2_sqr* call site squares a reduced value or one fp2_add_lazy): the values
+// stay below 20p, the column sums below 2^62.6 and the result below 2p (operand contract above).
+#ifndef BLS_FP2_SQR28
+#define BLS_FP2_SQR28 1
+#endif
+#if !BLS_FP2_SQR28
+// the r02 form (A/B): the sums as 12-word carry chains, then split
 DI u24 fp2_sqr_body(const u24& a) {
   const u12 a0 = u24_lo(a), a1 = u24_hi(a);
   uint32_t x[14], y[14];
@@ -433,6 +439,24 @@ DI u24 fp2_sqr_body(const u24& a) {
   const u12 c1 = fp_mont_dot<false>(x, y, x, y);
   return u24_of(c0, c1);
 }
+#else
+DI u24 fp2_sqr_body(const u24& a) {
+  uint32_t s0[14], s1[14], x[14], y[14];
+  fp_split28(u24_lo(a), s0);
+  fp_split28(u24_hi(a), s1);
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    x[k] = s0[k] + s1[k];
+    y[k] = s0[k] + (NEG28_16P[k] - s1[k]);
+  }
+  const u12 c0 = fp_mont_dot<false>(x, y, x, y);
+  BLS_SCHED_FENCE();
+#pragma unroll
+  for (int k = 0; k < 14; k++) x[k] = s0[k] << 1;
+  const u12 c1 = fp_mont_dot<false>(x, s1, x, s1);
+  return u24_of(c0, c1);
+}
+#endif
 
 // The called forms: b of fp2_mul_u24 comes from fp2_arg_store (LDS), one copy of each body per
 // code object. The _inl forms (tower.h fp2_mul_inl / fp2_sqr_inl) expand the bodies in place for
