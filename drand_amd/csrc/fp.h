@@ -551,7 +551,39 @@ DI fp fp_pow_words(const fp& a, const uint32_t (&e)[NW]) {
 NOINL u12 fp_pow_p_minus_2(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_2)); }
 NOINL u12 fp_pow_sqrt(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_PLUS_1_DIV_4)); }
 NOINL u12 fp_pow_legendre(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_1_DIV_2)); }
+#ifndef BLS_SQRT_W4
+#define BLS_SQRT_W4 1
+#endif
+#if BLS_SQRT_W4
+// a^((p-3)/4) by a 4-bit sliding window (bls_constants.h EXP_SQRT_W4, from gen_constants.py): the odd
+// powers a, a^3, ..., a^15 (8 values, 96 words: what the calling convention keeps across the calls),
+// 375 squarings and 78 multiplications instead of the fixed 2-bit windows' ~380 and ~143. The digit
+// of an entry is the same in every lane, so the table read is a wave-uniform select.
+NOINL u12 fp_pow_p_minus_3_div_4(u12 a12) {
+  const fp a = fp_from_u12(a12);
+  fp tab[8];
+  tab[0] = a;
+  const fp a2 = fp_sqr(a);
+#pragma unroll
+  for (int k = 1; k < 8; k++) tab[k] = fp_mul(tab[k - 1], a2);
+  fp r = tab[(EXP_SQRT_W4[0] & 255) >> 1];
+#pragma unroll 1
+  for (int e = 1; e < EXP_SQRT_W4_N; e++) {
+    const int ent = EXP_SQRT_W4[e], nsq = ent >> 8, d = (ent & 255) >> 1;
+#pragma unroll 1
+    for (int k = 0; k < nsq; k++) r = fp_sqr(r);
+    fp t = tab[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++) t = fp_select(d == k, tab[k], t);
+    r = fp_mul(r, t);
+  }
+#pragma unroll 1
+  for (int k = 0; k < EXP_SQRT_W4_TAIL; k++) r = fp_sqr(r);
+  return fp_to_u12(r);
+}
+#else
 NOINL u12 fp_pow_p_minus_3_div_4(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_3_DIV_4)); }
+#endif
 
 // w = a^((p-3)/4): t = w*a satisfies t^2 = a (a a residue or 0) or t^2 = -a (non-residue), and
 // 1/t = w or -w respectively: a square root AND its inverse from one exponentiation.
