@@ -272,10 +272,9 @@ NOINL u12 fp_mul_u12(u12 a, u12 b) {
 
 // Montgomery square: the cross products x_j x_{k-j} (j < k-j) appear twice, so they are taken once
 // against the doubled limbs 2x (29 bits, products < 2^57): 105 product MADs instead of 196.
-NOINL u12 fp_sqr_u12(u12 a) {
-  BLS_COUNT_MUL();
-  uint32_t x[14], x2[14], m[14], t[14];
-  fp_split28(a, x);
+// the square's column loop on split limbs x (< 2^28): t = x^2 R^-1 as 14 limbs (< 2^28, top < 2^18)
+DI void fp_sqr28_t(const uint32_t (&x)[14], uint32_t (&t)[14]) {
+  uint32_t x2[14], m[14];
 #pragma unroll
   for (int k = 0; k < 14; k++) x2[k] = x[k] << 1;
   uint64_t acc = 0;
@@ -298,6 +297,13 @@ NOINL u12 fp_sqr_u12(u12 a) {
     }
   }
   t[13] = (uint32_t)acc;
+}
+
+NOINL u12 fp_sqr_u12(u12 a) {
+  BLS_COUNT_MUL();
+  uint32_t x[14], t[14];
+  fp_split28(a, x);
+  fp_sqr28_t(x, t);
   return fp_join28(t);
 }
 
@@ -332,9 +338,9 @@ typedef uint32_t u24 __attribute__((ext_vector_type(24)));
 // below 2^29 (operand contract above fp_mul_u12):
 //   DOT:  r = (x0 y0 + x1 y1) R^-1        !DOT: r = x0 y0 R^-1         (r < 2p)
 template <bool DOT>
-DI u12 fp_mont_dot(const uint32_t (&x0)[14], const uint32_t (&y0)[14], const uint32_t (&x1)[14],
-                   const uint32_t (&y1)[14]) {
-  uint32_t m[14], t[14];
+DI void fp_mont_dot_t(const uint32_t (&x0)[14], const uint32_t (&y0)[14], const uint32_t (&x1)[14],
+                      const uint32_t (&y1)[14], uint32_t (&t)[14]) {
+  uint32_t m[14];
   uint64_t c = 0;
 #pragma unroll
   for (int k = 0; k < 27; k++) {
@@ -357,6 +363,46 @@ DI u12 fp_mont_dot(const uint32_t (&x0)[14], const uint32_t (&y0)[14], const uin
     c >>= 28;
   }
   t[13] = (uint32_t)c;
+}
+// x0 y0 + x1 y1 + x2 y2 (NT = 3) or the first two (NT = 2), one reduction: limbs below 2^29 (operand
+// splits and NEG28_4P negations of values < 2p), so a column holds at most 42 products < 2^58 plus 14
+// m_j p_{k-j} < 2^56 and the carry: < 2^63.5. Values: three terms below 24 p^2 each keep the result
+// below 2p (operand contract above fp_mul_u12).
+template <int NT>
+DI u12 fp_mont_dot3(const uint32_t (&x0)[14], const uint32_t (&y0)[14], const uint32_t (&x1)[14],
+                    const uint32_t (&y1)[14], const uint32_t (&x2)[14], const uint32_t (&y2)[14]) {
+  uint32_t m[14], t[14];
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    const int lo = k > 13 ? k - 13 : 0, hi = k < 13 ? k : 13;
+#pragma unroll
+    for (int j = lo; j <= hi; j++) {
+      c += (uint64_t)x0[j] * y0[k - j];
+      c += (uint64_t)x1[j] * y1[k - j];
+      if (NT == 3) c += (uint64_t)x2[j] * y2[k - j];
+    }
+    if (k < 14) {
+#pragma unroll
+      for (int j = 0; j < k; j++) c += (uint64_t)m[j] * P28[k - j];
+      m[k] = ((uint32_t)c * P_INV28) & M28;
+      c += (uint64_t)m[k] * P28[0];
+    } else {
+#pragma unroll
+      for (int j = k - 13; j < 14; j++) c += (uint64_t)m[j] * P28[k - j];
+      t[k - 14] = (uint32_t)c & M28;
+    }
+    c >>= 28;
+  }
+  t[13] = (uint32_t)c;
+  return fp_join28(t);
+}
+
+template <bool DOT>
+DI u12 fp_mont_dot(const uint32_t (&x0)[14], const uint32_t (&y0)[14], const uint32_t (&x1)[14],
+                   const uint32_t (&y1)[14]) {
+  uint32_t t[14];
+  fp_mont_dot_t<DOT>(x0, y0, x1, y1, t);
   return fp_join28(t);
 }
 
@@ -555,6 +601,34 @@ NOINL u12 fp_pow_legendre(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12
 #define BLS_SQRT_W4 1
 #endif
 #if BLS_SQRT_W4
+// Montgomery square / product with the running value kept split in radix 2^28 (14 limbs < 2^28, the
+// output form of the column loops): an exponentiation's chain of squares skips fp_split28 /
+// fp_join28 at every step
+typedef uint32_t u14 __attribute__((ext_vector_type(14)));
+NOINL u14 fp_sqr_r28(u14 xv) {
+  BLS_COUNT_MUL();
+  uint32_t x[14], t[14];
+#pragma unroll
+  for (int k = 0; k < 14; k++) x[k] = xv[k];
+  fp_sqr28_t(x, t);
+  u14 r;
+#pragma unroll
+  for (int k = 0; k < 14; k++) r[k] = t[k];
+  return r;
+}
+NOINL u14 fp_mul_r28(u14 xv, u12 b) {
+  BLS_COUNT_MUL();
+  uint32_t x[14], y[14], t[14];
+#pragma unroll
+  for (int k = 0; k < 14; k++) x[k] = xv[k];
+  fp_split28(b, y);
+  fp_mont_dot_t<false>(x, y, x, y, t);
+  u14 r;
+#pragma unroll
+  for (int k = 0; k < 14; k++) r[k] = t[k];
+  return r;
+}
+
 // a^((p-3)/4) by a 4-bit sliding window (bls_constants.h EXP_SQRT_W4, from gen_constants.py): the odd
 // powers a, a^3, ..., a^15 (8 values, 96 words: what the calling convention keeps across the calls),
 // 375 squarings and 78 multiplications instead of the fixed 2-bit windows' ~380 and ~143. The digit
@@ -566,20 +640,29 @@ NOINL u12 fp_pow_p_minus_3_div_4(u12 a12) {
   const fp a2 = fp_sqr(a);
 #pragma unroll
   for (int k = 1; k < 8; k++) tab[k] = fp_mul(tab[k - 1], a2);
-  fp r = tab[(EXP_SQRT_W4[0] & 255) >> 1];
+  u14 r;
+  {
+    uint32_t x[14];
+    fp_split28(fp_to_u12(tab[(EXP_SQRT_W4[0] & 255) >> 1]), x);
+#pragma unroll
+    for (int k = 0; k < 14; k++) r[k] = x[k];
+  }
 #pragma unroll 1
   for (int e = 1; e < EXP_SQRT_W4_N; e++) {
     const int ent = EXP_SQRT_W4[e], nsq = ent >> 8, d = (ent & 255) >> 1;
 #pragma unroll 1
-    for (int k = 0; k < nsq; k++) r = fp_sqr(r);
+    for (int k = 0; k < nsq; k++) r = fp_sqr_r28(r);
     fp t = tab[0];
 #pragma unroll
     for (int k = 1; k < 8; k++) t = fp_select(d == k, tab[k], t);
-    r = fp_mul(r, t);
+    r = fp_mul_r28(r, fp_to_u12(t));
   }
 #pragma unroll 1
-  for (int k = 0; k < EXP_SQRT_W4_TAIL; k++) r = fp_sqr(r);
-  return fp_to_u12(r);
+  for (int k = 0; k < EXP_SQRT_W4_TAIL; k++) r = fp_sqr_r28(r);
+  uint32_t t[14];
+#pragma unroll
+  for (int k = 0; k < 14; k++) t[k] = r[k];
+  return fp_join28(t);
 }
 #else
 NOINL u12 fp_pow_p_minus_3_div_4(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_3_DIV_4)); }
