@@ -111,6 +111,16 @@ def test_host_build_inversion_matches_exponentiation(opcount_bin):
     assert r.returncode == 0 and out["bad"] == 0 and out["unconverged"] == 0 and out["structured"] > 2000, out
 
 
+
+def test_host_sqrt_window_and_fp2_sqr_fuzz(opcount_bin):
+    """The 4-bit sliding-window square-root exponentiation (radix-2^28 running value) equals the fixed
+    2-bit-window one, and the Fp2 square with radix-2^28 sums equals (a0 + a1)(a0 - a1), 2 a0 a1 from
+    Fp products, for reduced operands and lazy sums (< 4p), on the host build of fp.h."""
+    r = subprocess.run([opcount_bin, "powfuzz", "3000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout)
+    assert out["pow_mismatch"] == 0 and out["fp2_sqr_mismatch"] == 0, out
+
 def _split_top(args):
     out, depth, cur = [], 0, ""
     for ch in args:

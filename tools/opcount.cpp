@@ -137,8 +137,47 @@ static int cmd_invfuzz(unsigned long n) {
   return bad != 0 || unconverged != 0;
 }
 
+// The square-root exponentiation (4-bit window, radix-2^28 running value) against the generic fixed-
+// window one, and the Fp2 square (radix-2^28 sums) against Fp products, on random inputs including
+// lazy sums (< 4p) as the callers pass them. Prints the mismatch count.
+static int cmd_powfuzz(unsigned long n) {
+  using namespace bls;
+  unsigned long long s = 0x2545f4914f6cdd1dull;
+  auto next = [&]() {
+    s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+    return (uint32_t)(s >> 11);
+  };
+  auto rnd2p = [&]() {  // a value < 2^381 < 2p (2p's top word is 0x340223d4)
+    fp x;
+    for (int i = 0; i < 12; i++) x.l[i] = next();
+    x.l[11] &= 0x1fffffffu;
+    return x;
+  };
+  unsigned long bad_pow = 0, bad_sqr = 0;
+  for (unsigned long t = 0; t < n; t++) {
+    fp x = rnd2p();
+    if (t == 0) x = fp_zero();
+    if (t == 1) x = fp_one();
+    const fp w = fp_from_u12(fp_pow_p_minus_3_div_4(fp_to_u12(x)));
+    const fp ref = fp_pow_words<12>(x, EXP_P_MINUS_3_DIV_4);
+    bad_pow += !fp_eq(w, ref);
+    // Fp2 square of a reduced value and of a lazy sum
+    const fp2 a = {rnd2p(), rnd2p()}, b = {rnd2p(), rnd2p()};
+    for (int lazy = 0; lazy < 2; lazy++) {
+      const fp2 in = lazy ? fp2_add_lazy(a, b) : a;
+      const fp2 red = lazy ? fp2_add(a, b) : a;
+      const fp2 got = fp2_sqr(in);
+      const fp2 want = {fp_mul(fp_add(red.c0, red.c1), fp_sub(red.c0, red.c1)), fp_dbl(fp_mul(red.c0, red.c1))};
+      bad_sqr += !fp2_eq(got, want);
+    }
+  }
+  printf("{\"inputs\": %lu, \"pow_mismatch\": %lu, \"fp2_sqr_mismatch\": %lu}\n", n, bad_pow, bad_sqr);
+  return (bad_pow || bad_sqr) ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
   if (argc == 3 && !strcmp(argv[1], "hash")) return cmd_hash(argv[2]);
+  if (argc == 3 && !strcmp(argv[1], "powfuzz")) return cmd_powfuzz(strtoul(argv[2], nullptr, 10));
   if (argc == 3 && !strcmp(argv[1], "invfuzz")) return cmd_invfuzz(strtoul(argv[2], nullptr, 10));
   if (argc != 5) {
     fprintf(stderr, "usage: %s pk48hex round prevhex|- sig96hex   (prev '-' = unchained V2)\n       %s hash msghex\n",
