@@ -600,6 +600,9 @@ NOINL u12 fp_pow_legendre(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12
 #ifndef BLS_SQRT_W4
 #define BLS_SQRT_W4 1
 #endif
+#ifndef BLS_SQRT_SQR_INL
+#define BLS_SQRT_SQR_INL 1
+#endif
 #if BLS_SQRT_W4
 // Montgomery square / product with the running value kept split in radix 2^28 (14 limbs < 2^28, the
 // output form of the column loops): an exponentiation's chain of squares skips fp_split28 /
@@ -651,7 +654,18 @@ NOINL u12 fp_pow_p_minus_3_div_4(u12 a12) {
   for (int e = 1; e < EXP_SQRT_W4_N; e++) {
     const int ent = EXP_SQRT_W4[e], nsq = ent >> 8, d = (ent & 255) >> 1;
 #pragma unroll 1
-    for (int k = 0; k < nsq; k++) r = fp_sqr_r28(r);
+    for (int k = 0; k < nsq; k++) {
+#if BLS_SQRT_SQR_INL
+      uint32_t x[14], tt[14];
+#pragma unroll
+      for (int q = 0; q < 14; q++) x[q] = r[q];
+      fp_sqr28_t(x, tt);
+#pragma unroll
+      for (int q = 0; q < 14; q++) r[q] = tt[q];
+#else
+      r = fp_sqr_r28(r);
+#endif
+    }
     fp t = tab[0];
 #pragma unroll
     for (int k = 1; k < 8; k++) t = fp_select(d == k, tab[k], t);

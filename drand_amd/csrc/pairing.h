@@ -57,7 +57,36 @@ DI void miller_dbl_step(g2proj& t, fp2& l00, fp2& l01, fp2& l11, const fp& xp, c
 // in place, one after the other (fenced), ordered so that few values are live at once, and each
 // line coefficient handed to put(c, v) (c = 0: l00, 1: l01, 2: l11) as soon as it is known; xp()/yp()
 // and the addition's q() re-read their operands at the use. Same operations on the same values as
-// miller_dbl_step / miller_add_step, so the lines are bit-identical.
+// miller_dbl_step / miller_add_step (BLS_LINES_FOLD: 3 xP, -yP and -xP folded into the radix-2^28
+// operand, the same residues in possibly another representative below 2p).
+#ifndef BLS_LINES_FOLD
+#define BLS_LINES_FOLD 0  // A/B profiles/r03s_lines_fold_sqrt_inl_ab.json: ~1 ms slower (scratch 504 -> 516 B)
+#endif
+// a * b for b handed over as radix-2^28 limbs that the caller has scaled by 3 or negated limb-wise
+// (fp_neg28: 16p - b): the line coefficients 3 X^2 xP, -H yP and -theta xP then cost no Fp2 mul3 or
+// negation. Limbs < 3 * 2^28 keep every column sum of fp_mont_dot below 2^63, and a product of
+// values < 2p and < 16p is < 2p after the reduction (R = 2^392), as fp2_mul's negated operand is.
+DI fp2 fp2_mul_fp28_inl(const fp2& a, const uint32_t (&y)[14]) {
+  BLS_COUNT_MUL();
+  BLS_COUNT_MUL();
+  uint32_t x[14];
+  fp_split28(fp_to_u12(a.c0), x);
+  const fp c0 = fp_from_u12(fp_mont_dot<false>(x, y, x, y));
+  BLS_SCHED_FENCE();
+  fp_split28(fp_to_u12(a.c1), x);
+  return {c0, fp_from_u12(fp_mont_dot<false>(x, y, x, y))};
+}
+DI void fp_split28_x3(const fp& a, uint32_t (&y)[14]) {
+  fp_split28(fp_to_u12(a), y);
+#pragma unroll
+  for (int k = 0; k < 14; k++) y[k] *= 3u;
+}
+DI void fp_split28_neg(const fp& a, uint32_t (&y)[14]) {
+  uint32_t v[14];
+  fp_split28(fp_to_u12(a), v);
+  fp_neg28(v, y);
+}
+
 template <typename Put, typename XP, typename YP>
 DI void miller_dbl_step_inl(g2proj& t, Put put, XP xp, YP yp) {
   const fp2 B = fp2_sqr_inl(t.y);
@@ -66,7 +95,15 @@ DI void miller_dbl_step_inl(g2proj& t, Put put, XP xp, YP yp) {
   BLS_SCHED_FENCE();
   const fp2 H = fp2_sub(fp2_sqr_inl(fp2_add_lazy(t.y, t.z)), fp2_add(B, C));
   BLS_SCHED_FENCE();
+#if BLS_LINES_FOLD
+  {
+    uint32_t y[14];
+    fp_split28_neg(yp(), y);
+    put(2, fp2_mul_fp28_inl(H, y));
+  }
+#else
   put(2, fp2_neg(fp2_mul_fp_inl(H, yp())));
+#endif
   BLS_SCHED_FENCE();
   const fp2 Z3 = fp2_mul_inl(B, H);
   BLS_SCHED_FENCE();
@@ -79,7 +116,16 @@ DI void miller_dbl_step_inl(g2proj& t, Put put, XP xp, YP yp) {
   BLS_SCHED_FENCE();
   const fp2 X3 = fp2_mul_inl(A, BF);
   BLS_SCHED_FENCE();
+#if BLS_LINES_FOLD
+  {
+    const fp2 X2 = fp2_sqr_inl(t.x);
+    uint32_t y[14];
+    fp_split28_x3(xp(), y);
+    put(1, fp2_mul_fp28_inl(X2, y));
+  }
+#else
   put(1, fp2_mul_fp_inl(fp2_mul3(fp2_sqr_inl(t.x)), xp()));
+#endif
   BLS_SCHED_FENCE();
   const fp2 G2 = fp2_sqr_inl(G);
   BLS_SCHED_FENCE();
@@ -101,9 +147,20 @@ DI void miller_add_step_inl(g2proj& t, Q qload, Put put, XP xp, YP yp) {
     put(0, fp2_sub(u, fp2_mul_inl(delta, q.y)));
     BLS_SCHED_FENCE();
   }
+#if BLS_LINES_FOLD
+  {
+    uint32_t y[14];
+    fp_split28_neg(xp(), y);
+    put(1, fp2_mul_fp28_inl(theta, y));
+    BLS_SCHED_FENCE();
+    fp_split28(fp_to_u12(yp()), y);
+    put(2, fp2_mul_fp28_inl(delta, y));
+  }
+#else
   put(1, fp2_neg(fp2_mul_fp_inl(theta, xp())));
   BLS_SCHED_FENCE();
   put(2, fp2_mul_fp_inl(delta, yp()));
+#endif
   BLS_SCHED_FENCE();
   const fp2 C = fp2_sqr_inl(theta);
   BLS_SCHED_FENCE();
