@@ -656,6 +656,7 @@ NOINL u12 fp_pow_p_minus_3_div_4(u12 a12) {
 #pragma unroll 1
     for (int k = 0; k < nsq; k++) {
 #if BLS_SQRT_SQR_INL
+      BLS_COUNT_MUL();
       uint32_t x[14], tt[14];
 #pragma unroll
       for (int q = 0; q < 14; q++) x[q] = r[q];
