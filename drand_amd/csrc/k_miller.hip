@@ -16,6 +16,33 @@ DI int line_slot(int step, int k) { return (step * 2 + k) * 6; }
 // The two pairs run in separate workgroups (k = blockIdx.x & 1: the pair of the whole wave), so a
 // beacon's two line chains run side by side: half the latency of one lane walking both, twice the
 // waves (a finer tail), and every store still one 256-byte access per wave.
+#ifndef BLS_LINES_T_LDS
+#define BLS_LINES_T_LDS 1
+#endif
+#if BLS_LINES_INL == 2 && BLS_LINES_T_LDS
+static __shared__ uint32_t g_ml_T[72 * BLS_LANES];
+// T = (X, Y, Z) in LDS, word w of coordinate c at [(24 c + w) * 64 + lane]: conflict-free dword access
+struct g2proj_lds {
+  uint32_t* base;
+  DI fp2 get(int c) const {
+    fp2 v;
+#pragma unroll
+    for (int w = 0; w < 12; w++) {
+      v.c0.l[w] = base[(24 * c + w) * BLS_LANES];
+      v.c1.l[w] = base[(24 * c + 12 + w) * BLS_LANES];
+    }
+    return v;
+  }
+  DI void set(int c, const fp2& v) const {
+#pragma unroll
+    for (int w = 0; w < 12; w++) {
+      base[(24 * c + w) * BLS_LANES] = v.c0.l[w];
+      base[(24 * c + 12 + w) * BLS_LANES] = v.c1.l[w];
+    }
+  }
+};
+#endif
+
 BLS_KERNEL(BLS_WPE_LINES)
 k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
                const uint8_t* h_inf, const uint32_t* S, const uint8_t* s_inf, const uint8_t* cls, size_t cnt,
@@ -60,17 +87,30 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
     auto put = [&](int c, const fp2& v) { st_fp2(LN, sub, i, line_slot(step, k) + 2 * c, v); };
     auto xp = [&]() { return pcoord(0); };
     auto yp = [&]() { return pcoord(1); };
-    g2proj T;
+#if BLS_LINES_T_LDS
+    // T parks in LDS (72 words per lane, word-major: 18 KB per one-wave workgroup, 8 per CU at 2
+    // waves/SIMD), read at each use and written back coordinate by coordinate
+    const g2proj_lds T{g_ml_T + threadIdx.x};
     {
       const g2a Q0 = load_q();
-      T = {Q0.x, Q0.y, fp2_one()};
+      T.set(0, Q0.x);
+      T.set(1, Q0.y);
+      T.set(2, fp2_one());
     }
+#else
+    g2proj Tr;
+    {
+      const g2a Q0 = load_q();
+      Tr = {Q0.x, Q0.y, fp2_one()};
+    }
+    const g2proj_reg T{Tr};
+#endif
 #pragma unroll 1
     for (int b = 62; b >= 0; b--) {
-      miller_dbl_step_inl(T, put, xp, yp);
+      miller_dbl_step_ts(T, put, xp, yp);
       step++;
       if ((BLS_X_ABS >> b) & 1ull) {
-        miller_add_step_inl(T, load_q, put, xp, yp);
+        miller_add_step_ts(T, load_q, put, xp, yp);
         step++;
       }
     }

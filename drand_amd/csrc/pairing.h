@@ -87,13 +87,27 @@ DI void fp_split28_neg(const fp& a, uint32_t (&y)[14]) {
   fp_neg28(v, y);
 }
 
-template <typename Put, typename XP, typename YP>
-DI void miller_dbl_step_inl(g2proj& t, Put put, XP xp, YP yp) {
-  const fp2 B = fp2_sqr_inl(t.y);
+// The running point T of the call-free steps is reached through an accessor: TS::get(c) / set(c, v)
+// for c = 0, 1, 2 (X, Y, Z). TReg keeps T in registers; k_miller_lines parks it in LDS (its
+// register budget at 2 waves/SIMD is then left to the products). Each coordinate is written back as
+// soon as its old value has had its last use.
+struct g2proj_reg {
+  g2proj& t;
+  DI fp2 get(int c) const { return c == 0 ? t.x : c == 1 ? t.y : t.z; }
+  DI void set(int c, const fp2& v) const {
+    if (c == 0) t.x = v;
+    else if (c == 1) t.y = v;
+    else t.z = v;
+  }
+};
+
+template <typename TS, typename Put, typename XP, typename YP>
+DI void miller_dbl_step_ts(const TS& t, Put put, XP xp, YP yp) {
+  const fp2 B = fp2_sqr_inl(t.get(1));
   BLS_SCHED_FENCE();
-  const fp2 C = fp2_sqr_inl(t.z);
+  const fp2 C = fp2_sqr_inl(t.get(2));
   BLS_SCHED_FENCE();
-  const fp2 H = fp2_sub(fp2_sqr_inl(fp2_add_lazy(t.y, t.z)), fp2_add(B, C));
+  const fp2 H = fp2_sub(fp2_sqr_inl(fp2_add_lazy(t.get(1), t.get(2))), fp2_add(B, C));
   BLS_SCHED_FENCE();
 #if BLS_LINES_FOLD
   {
@@ -105,42 +119,41 @@ DI void miller_dbl_step_inl(g2proj& t, Put put, XP xp, YP yp) {
   put(2, fp2_neg(fp2_mul_fp_inl(H, yp())));
 #endif
   BLS_SCHED_FENCE();
-  const fp2 Z3 = fp2_mul_inl(B, H);
+  t.set(2, fp2_mul_inl(B, H));  // Z3 (Z has had its last use)
   BLS_SCHED_FENCE();
   const fp2 E = fp2_mul_3b(C);
   const fp2 F = fp2_mul3(E);
   const fp2 G = fp2_half(fp2_add(B, F));
   put(0, fp2_sub(E, B));
   const fp2 BF = fp2_sub(B, F);
-  const fp2 A = fp2_half(fp2_mul_inl(t.x, t.y));
-  BLS_SCHED_FENCE();
-  const fp2 X3 = fp2_mul_inl(A, BF);
+  const fp2 A = fp2_half(fp2_mul_inl(t.get(0), t.get(1)));
   BLS_SCHED_FENCE();
 #if BLS_LINES_FOLD
   {
-    const fp2 X2 = fp2_sqr_inl(t.x);
+    const fp2 X2 = fp2_sqr_inl(t.get(0));
     uint32_t y[14];
     fp_split28_x3(xp(), y);
     put(1, fp2_mul_fp28_inl(X2, y));
   }
 #else
-  put(1, fp2_mul_fp_inl(fp2_mul3(fp2_sqr_inl(t.x)), xp()));
+  put(1, fp2_mul_fp_inl(fp2_mul3(fp2_sqr_inl(t.get(0))), xp()));
 #endif
+  BLS_SCHED_FENCE();
+  t.set(0, fp2_mul_inl(A, BF));  // X3
   BLS_SCHED_FENCE();
   const fp2 G2 = fp2_sqr_inl(G);
   BLS_SCHED_FENCE();
-  const fp2 Y3 = fp2_sub(G2, fp2_mul3(fp2_sqr_inl(E)));
-  t = {X3, Y3, Z3};
+  t.set(1, fp2_sub(G2, fp2_mul3(fp2_sqr_inl(E))));  // Y3
 }
 
-template <typename Put, typename Q, typename XP, typename YP>
-DI void miller_add_step_inl(g2proj& t, Q qload, Put put, XP xp, YP yp) {
+template <typename TS, typename Put, typename Q, typename XP, typename YP>
+DI void miller_add_step_ts(const TS& t, Q qload, Put put, XP xp, YP yp) {
   fp2 theta, delta;
   {
     const g2a q = qload();
-    theta = fp2_sub(t.y, fp2_mul_inl(q.y, t.z));
+    theta = fp2_sub(t.get(1), fp2_mul_inl(q.y, t.get(2)));
     BLS_SCHED_FENCE();
-    delta = fp2_sub(t.x, fp2_mul_inl(q.x, t.z));
+    delta = fp2_sub(t.get(0), fp2_mul_inl(q.x, t.get(2)));
     BLS_SCHED_FENCE();
     const fp2 u = fp2_mul_inl(theta, q.x);
     BLS_SCHED_FENCE();
@@ -168,17 +181,25 @@ DI void miller_add_step_inl(g2proj& t, Q qload, Put put, XP xp, YP yp) {
   BLS_SCHED_FENCE();
   const fp2 E = fp2_mul_inl(D, delta);
   BLS_SCHED_FENCE();
-  const fp2 F = fp2_mul_inl(t.z, C);
+  const fp2 F = fp2_mul_inl(t.get(2), C);
   BLS_SCHED_FENCE();
-  const fp2 G = fp2_mul_inl(t.x, D);
+  const fp2 G = fp2_mul_inl(t.get(0), D);
   BLS_SCHED_FENCE();
   const fp2 H = fp2_sub(fp2_add(E, F), fp2_dbl(G));
-  const fp2 X3 = fp2_mul_inl(delta, H);
+  t.set(0, fp2_mul_inl(delta, H));  // X3 (X has had its last use)
   BLS_SCHED_FENCE();
-  const fp2 Y3 = fp2_sub(fp2_mul_inl(theta, fp2_sub(G, H)), fp2_mul_inl(t.y, E));
+  t.set(1, fp2_sub(fp2_mul_inl(theta, fp2_sub(G, H)), fp2_mul_inl(t.get(1), E)));  // Y3
   BLS_SCHED_FENCE();
-  const fp2 Z3 = fp2_mul_inl(t.z, E);
-  t = {X3, Y3, Z3};
+  t.set(2, fp2_mul_inl(t.get(2), E));  // Z3
+}
+
+template <typename Put, typename XP, typename YP>
+DI void miller_dbl_step_inl(g2proj& t, Put put, XP xp, YP yp) {
+  miller_dbl_step_ts(g2proj_reg{t}, put, xp, yp);
+}
+template <typename Put, typename Q, typename XP, typename YP>
+DI void miller_add_step_inl(g2proj& t, Q qload, Put put, XP xp, YP yp) {
+  miller_add_step_ts(g2proj_reg{t}, qload, put, xp, yp);
 }
 
 DI void miller_add_step(g2proj& t, const g2a& q, fp2& l00, fp2& l01, fp2& l11, const fp& xp, const fp& yp) {
