@@ -1,0 +1,13 @@
+# G2 [x] chains with the accumulator's X, Y parked in LDS (variants/lds: BLS_G2_ACC_LDS=1) vs in registers
+# (main): GPU suite on the lds variant, same-box A/B
+set -o pipefail
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r03y
+mkdir -p $O
+DRAND_AMD_LIB=$PWD/variants/libblsverify_lds.so timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit 12
+for v in lds main lds main; do
+  lib=$PWD/drand_amd/libblsverify.so; [ $v = main ] || lib=$PWD/variants/libblsverify_$v.so
+  DRAND_AMD_LIB=$lib timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --cpu-per-worker 0 >> $O/bench_$v.json 2>> $O/bench_$v.err || exit 13
+done
+echo done
