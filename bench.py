@@ -18,22 +18,31 @@ process (the 12.5M-round slice of configs[3] on one GPU).
 
 One step = one blsv_verify_chained_dev call over the rank's whole HBM-resident shard (hash-to-G2,
 decompress + subgroup, 2-pair Miller loop, final exponentiation, verdict bitmap + first bad round),
-followed for N>1 by the exchange: an all-reduce MIN of first_bad and an all-gather of the per-shard
-verdict bitmaps over RCCL (re-packed to global bit positions on the device for unaligned shards).
+followed for N>1 by the exchange: ONE SUM all-reduce over RCCL of a zero-initialised buffer holding
+the verdict bits at global positions plus one first-bad-round slot per rank (shard.combine).
+
+Ranks: with --gpus N > 1 and no WORLD_SIZE in the environment, this process starts the N ranks
+itself as a child `python -m torch.distributed.run --nproc-per-node N ...` (before anything here
+touches the GPU) and exits with its status; every rank asserts world_size == --gpus. With
+--dist-backend gloo the exchange runs through host copies and ranks may share a GPU (rank r on
+cuda:(r mod device_count)) -- the -m gpu test runs 2 ranks on one MI355X that way.
 
 Correctness gate before timing: every round verifies, then a negative control -- one signature per
 rank corrupted (bit flip in x) must make exactly that round and the next one reject, with first_bad
 = the lowest corrupted round over all ranks.
 
 Usage: python bench.py [--gpus N --steps K --warmup W --n BEACONS_PER_GPU]
-       python bench.py --total-rounds 100000000 --slice 7/8
-       (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+       python bench.py --gpus 8 --total-rounds 100000000          (configs[3], 8 ranks over RCCL)
+       python bench.py --total-rounds 100000000 --slice 7/8      (one shard of it in one process)
+       (or launched per rank: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -102,19 +111,81 @@ def cpu_baseline(pk48, segments, workers):
     return n / dt, sum(oks), n
 
 
+def launch_ranks(n):
+    """Start n ranks of this script under torch.distributed.run as a CHILD process (never an exec:
+    this process has not touched the GPU, and the ranks must each initialise their own) and return
+    its exit status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    # torch.distributed.run's parser would take "--n" as an abbreviation of its own options
+    argv = ["--beacons-per-gpu" if a == "--n" else "--beacons-per-gpu=" + a[4:] if a.startswith("--n=") else a
+            for a in sys.argv[1:]]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + argv
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (the box's driver)
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(args, world, rank):
+    """--launch-check: the N-rank plumbing without a GPU (gloo on host tensors): process group of
+    --gpus ranks, then one shard.combine exchange of a synthetic verdict bitmap with one rejected
+    round in the last rank's shard."""
+    import torch
+    import torch.distributed as dist
+
+    from drand_amd import shard
+
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus
+    total = args.total_rounds or args.n * world
+    counts = [shard.shard_range(total, world, r).count for r in range(world)] if args.total_rounds else [args.n] * world
+    n = counts[rank]
+    bad = total - 2  # global index of the rejected round
+    start = sum(counts[:rank])
+    ok = [start + i != bad for i in range(n)]
+    words = [0] * ((n + 63) // 64)
+    for i, v in enumerate(ok):
+        words[i // 64] |= v << (i % 64)
+    w = torch.tensor([x - (1 << 64) if x >= 1 << 63 else x for x in words], dtype=torch.int64)
+    fb = start + 1 + ok.index(False) if False in ok else shard.NONE_U64
+    if world > 1:
+        fbv, gw = shard.combine(fb, w, n, counts=counts)
+    else:
+        fbv, gw = fb, words
+    print(json.dumps({"rank": rank, "world_size": world, "gpus": args.gpus, "counts": counts,
+                      "first_bad": fbv, "rejected": [i for i in range(total) if not (gw[i // 64] >> (i % 64)) & 1]}),
+          flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=1_000_000, help="beacons per GPU (configs[1]: 1M)")
+    ap.add_argument("--n", "--beacons-per-gpu", dest="n", type=int, default=1_000_000,
+                    help="beacons per GPU (configs[1]: 1M)")
     ap.add_argument("--total-rounds", type=int, default=0,
                     help="strong scaling (configs[3]): one history of this many rounds split over the ranks")
     ap.add_argument("--slice", default="", help="R/W: verify shard R of a W-way split in this one process")
     ap.add_argument("--seg-len", type=int, default=64, help="rounds per independently seeded chained segment")
     ap.add_argument("--cpu-per-worker", type=int, default=384, help="C-oracle beacons per host thread (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=0, help="host threads for the CPU baseline (0 = all usable cores)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="exchange backend for N>1: nccl (= RCCL over xGMI, one GPU per rank) or gloo (host "
+                         "copies; ranks may share a GPU)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, form the process group, run one exchange on host tensors and print "
+                         "one JSON line per rank, without touching a GPU (CPU test of the N-rank launch)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     import numpy as np
     import torch
@@ -123,13 +194,27 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: every rank must run with --gpus = "
+                         "the number of ranks")
+    if args.launch_check:
+        return launch_check(args, world, rank)
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if world > 1 and args.dist_backend == "nccl" and ndev < world:
+        raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs, this node shows {ndev} "
+                         "(--dist-backend gloo lets ranks share a GPU)")
+    dev_idx = local % max(ndev, 1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev_idx)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
 
     from drand_amd import shard
     from drand_amd.engine import Engine
@@ -178,7 +263,7 @@ def main():
     bitmap = torch.zeros(words, dtype=torch.int64, device=dev)
     first_bad = torch.empty(1, dtype=torch.int64, device=dev)
 
-    eng = Engine(local)
+    eng = Engine(dev_idx)
     eng.set_public_key(pk48)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
@@ -194,7 +279,7 @@ def main():
         eng.verify_chained_dev(first_round, seg, seeds.data_ptr(), seed0_len, sigs.data_ptr(), n,
                                bitmap.data_ptr(), first_bad.data_ptr(), None, sp, seg_phase=phase)
         if world > 1:
-            # per-shard first bad ROUND -> global min; per-shard bitmaps -> every rank (RCCL over xGMI)
+            # ONE SUM all-reduce: global-position bitmap + per-rank first bad ROUND slots (RCCL over xGMI)
             return shard.combine(first_bad, bitmap, n, to_host=False, counts=counts)
         return first_bad, bitmap
 
@@ -251,8 +336,8 @@ def main():
     dt = time.perf_counter() - t0
     prof = eng.profile_read()
     eng.profile(False)
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:  # the job's time is the slowest rank's
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -317,10 +402,19 @@ def main():
                 "the next round, first_bad = lowest corrupted round",
     }
     if world > 1:  # what the process group actually initialised (the exchange runs over it)
+        devs = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        if args.dist_backend == "gloo":
+            dist.all_gather(devs, torch.tensor([dev_idx]))
         out["dist"] = {"backend": str(dist.get_backend()), "world_size": dist.get_world_size(),
-                       "ranks_verified_rounds": sum(counts), "exchange": "all_reduce(MIN first_bad) + "
-                       "all_gather(bitmap words)" + (" + device word-shift repack" if any(c % 64 for c in counts[:-1])
-                                                       else "")}
+                       "rank_counts": counts, "ranks_verified_rounds": sum(counts),
+                       "exchange": "one all_reduce(SUM) of %d int64 words: the verdict bitmap at global bit "
+                                   "positions (disjoint bits: SUM = OR) + %d first-bad-round slots"
+                                   % ((sum(counts) + 63) // 64 + world, world),
+                       "gate": "passed"}
+        if args.dist_backend == "gloo":
+            out["dist"]["devices"] = [int(d) for d in devs]
+            if len({int(d) for d in devs}) < world:
+                out["dist"]["note"] = "ranks share a GPU: a correctness run of the N-rank path, not a scaling number"
     if rank == 0 and world == 1 and args.cpu_per_worker > 0 and not strong:  # CPU baseline: rank 0 at N=1 only
         # bounded sample of the same workload: the first whole segments of the rank-0 shard
         cores, host = host_cores()

@@ -197,7 +197,7 @@ def verify_store_sharded(engine, public_key: bytes, path, device=None, group=Non
 
     Each rank loads and verifies a contiguous slice of the stored entries (``shard.shard_range``).
     No halo is needed: every stored beacon carries its own PreviousSig. The exchange is
-    ``shard.combine``: one MIN all-reduce of the first bad round and one all-gather of the bitmaps.
+    ``shard.combine``: one SUM all-reduce of the global-position bitmap and the per-rank first bad rounds.
     Returns (global first bad round or None, global ok bool array in stored order)."""
     import torch
     import torch.distributed as dist

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -54,13 +55,24 @@ struct ProfRec {
   hipEvent_t a, b;
 };
 
-// Cutover between the latency path (one wave per item, k_lat.hip) and the batch pipeline: a batch of at
-// most this many items runs on the latency path. BLSV_LAT_MAX overrides it (0 = batch pipeline only).
+// Cutover between the latency path (one workgroup per item, k_lat.hip) and the batch pipeline: a batch
+// of at most this many items runs on the latency path. BLSV_LAT_MAX overrides it (0 = batch pipeline
+// only). Any value is clamped to kMaxChunk: the latency kernels write one class byte per item into the
+// chunk-sized class buffer, so a larger batch always takes the chunked pipeline.
 constexpr size_t kLatMaxDefault = 2048;
 static size_t lat_max_env() {
   static const size_t v = [] {
     const char* e = getenv("BLSV_LAT_MAX");
-    return e ? (size_t)strtoull(e, nullptr, 10) : kLatMaxDefault;
+    if (!e) return kLatMaxDefault;
+    char* end = nullptr;
+    errno = 0;
+    const unsigned long long x = strtoull(e, &end, 10);
+    if (end == e || *end != '\0' || errno == ERANGE || e[0] == '-') {
+      fprintf(stderr, "blsverify: ignoring BLSV_LAT_MAX=\"%s\" (not a non-negative integer); cutover stays %zu\n", e,
+              kLatMaxDefault);
+      return kLatMaxDefault;
+    }
+    return (size_t)std::min<unsigned long long>(x, kMaxChunk);
   }();
   return v;
 }
@@ -293,7 +305,8 @@ static int run_lat(blsv_ctx* c, size_t n, LatFn lat, uint64_t* d_bitmap, unsigne
   return BLSV_OK;
 }
 
-static bool use_lat(const blsv_ctx* c, size_t n) { return n > 0 && n <= c->lat_max; }
+// lat_max is clamped to kMaxChunk on every path that sets it; the min keeps the bound local anyway
+static bool use_lat(const blsv_ctx* c, size_t n) { return n > 0 && n <= std::min(c->lat_max, kMaxChunk); }
 
 struct NoLat {
   void operator()(uint8_t*) const {}
@@ -983,7 +996,7 @@ int blsv_profile_read(blsv_ctx* c, double* ms, uint64_t* launches, uint64_t* ite
 size_t blsv_set_lat_max(blsv_ctx* c, size_t lat_max) {
   if (!c) return 0;
   const size_t prev = c->lat_max;
-  c->lat_max = lat_max;
+  c->lat_max = std::min(lat_max, kMaxChunk);  // see lat_max_env: larger batches take the pipeline
   return prev;
 }
 

@@ -240,12 +240,14 @@ class Engine:
     def aggregate_round(self, msg1, partials1, msg2, partials2, t, n):
         """The aggregation step of one round cache, V1 + V2 (blsv_aggregate_round, chain.go:131-166):
         returns (status AGG_*, ok1, ok2, sig1, sig2 or None, v2_valid)."""
-        # a share of the wrong length cannot parse: kyber's Recover skips it and VerifyPartial rejects
-        # it, so it is dropped here (ok = False at its position) instead of failing the whole round
-        all1, all2 = [bytes(p) for p in partials1], [bytes(p) for p in partials2]
-        at1 = [i for i, p in enumerate(all1) if len(p) == 98]
-        at2 = [i for i, p in enumerate(all2) if len(p) == 98]
-        partials1, partials2 = [all1[i] for i in at1], [all2[i] for i in at2]
+        # A share of the wrong length cannot parse: kyber's Recover skips it and VerifyPartial rejects
+        # it, but it still counts in roundCache.Len()/LenV2() -- the V2 gate `LenV2() >= thr`
+        # (chain.go:153) sees it. So it is passed on as a 98-byte share that can never verify (index
+        # 0xFFFF >= n, compression flag clear): the C side counts it toward k2 >= t, rejects it
+        # (ok = False at its position) and Recover skips it, exactly as kyber does.
+        bad_share = b"\xff\xff" + bytes(96)
+        partials1 = [p if len(p) == 98 else bad_share for p in (bytes(p) for p in partials1)]
+        partials2 = [p if len(p) == 98 else bad_share for p in (bytes(p) for p in partials2)]
         k1, k2 = len(partials1), len(partials2)
         plen = 98
         ok1, ok2 = _lib.out_buf(k1), _lib.out_buf(k2)
@@ -253,18 +255,15 @@ class Engine:
         st = ctypes.c_int32()
         v2 = _lib.out_buf(1)
         self._check(self.lib.blsv_aggregate_round(
-            self._h, _lib.buf(msg1), len(msg1), _lib.buf(b"".join(bytes(p) for p in partials1)), k1,
-            _lib.buf(msg2), len(msg2), _lib.buf(b"".join(bytes(p) for p in partials2)), k2, plen, t, n, ok1, ok2,
+            self._h, _lib.buf(msg1), len(msg1), _lib.buf(b"".join(partials1)), k1,
+            _lib.buf(msg2), len(msg2), _lib.buf(b"".join(partials2)), k2, plen, t, n, ok1, ok2,
             s1, s2, ctypes.byref(st), v2))
         status = st.value
         sig1 = bytes(s1) if status in (_lib.AGG_OK, _lib.AGG_OK_V2, _lib.AGG_V1_INVALID,
                                        _lib.AGG_V2_RECOVER_FAIL) else None
         sig2 = bytes(s2) if status == _lib.AGG_OK_V2 else None
-        r1, r2 = [False] * len(all1), [False] * len(all2)
-        for j, i in enumerate(at1):
-            r1[i] = bool(ok1[j])
-        for j, i in enumerate(at2):
-            r2[i] = bool(ok2[j])
+        r1 = [bool(x) for x in list(ok1)[:k1]]
+        r2 = [bool(x) for x in list(ok2)[:k2]]
         return status, r1, r2, sig1, sig2, bool(v2[0])
 
     def sign(self, sk32, msgs, index=-1):

@@ -4,13 +4,10 @@ Each rank verifies a contiguous range of rounds. A beacon's verdict depends only
 PreviousSig bytes, Signature, pk) -- chain.VerifyBeacon, chain/beacon.go:87-92 -- so the only data
 a shard needs from outside its range is a one-signature halo: the signature of the round just
 before it, or the genesis seed (GroupHash, client/verify.go:122-124) for the shard that starts at
-round 1. After the local verification one exchange combines the results (torch.distributed; the
-"nccl" backend is RCCL over xGMI on MI355X, "gloo" in the CPU tests):
-
-  * all-reduce MIN of the per-shard first bad ROUND (UINT64_MAX = none is mapped to INT64_MAX so
-    that signed MIN is correct);
-  * all-gather of the per-shard verdict bitmaps (RCCL has no bitwise OR; shards are disjoint, so
-    gathering is exact), re-packed to global bit positions when a shard is not 64-aligned.
+round 1. After the local verification ONE collective combines the results (torch.distributed;
+the "nccl" backend is RCCL over xGMI on MI355X, "gloo" in the CPU tests): a SUM all-reduce of a
+zero-initialised buffer holding the global-position verdict bitmap plus one first-bad-round slot per
+rank (``combine``).
 """
 from __future__ import annotations
 
@@ -86,57 +83,92 @@ def from_i64_first_bad(v: int) -> int:
 
 
 def combine(first_bad, bitmap_words, count: int, group=None, to_host: bool = True, counts=None):
-    """Exchange step of the sharded verification (call on every rank).
+    """Exchange step of the sharded verification (call on every rank): ONE all-reduce.
+
+    Every rank writes its verdict bits at their GLOBAL positions into a zero-initialised buffer of
+    ceil(total/64) words, followed by one slot per rank holding that rank's first bad round
+    (INT64_MAX = none) and zeros in the other ranks' slots. One SUM all-reduce of that buffer then
+    gives every rank the whole bitmap and every shard's first bad round: the shards' bits are
+    disjoint (a word shared by two shards at an unaligned boundary gets bits from both), and adding
+    integers with disjoint set bits never carries, so SUM is exactly OR (RCCL has no bitwise OR).
+    The global first bad round is the MIN over the slots, taken locally.
 
     first_bad: this shard's first rejected ROUND -- a Python int (NONE_U64 = none) or a 1-element
       int64 device tensor as written by blsv_verify_chained_dev (UINT64_MAX reads back as -1).
-    bitmap_words: this shard's verdict bitmap, a 1-D int64 tensor of ceil(count/64) words (bit i =
-      the shard's i-th beacon, LSB first) on the device the process group uses.
-    counts: every rank's shard length, when the caller knows them (shard_range); else one extra
-      all-gather of the lengths.
+    bitmap_words: this shard's verdict bitmap, a 1-D int64 tensor of >= ceil(count/64) words (bit i
+      = the shard's i-th beacon, LSB first; bits past ``count`` are ignored).
+    counts: every rank's shard length when the caller knows them (shard_range); else one small
+      all-gather of the lengths first (not on the bench path).
+    With the gloo backend and a device tensor (two ranks sharing one GPU in the tests) the buffer is
+    all-reduced through a host copy.
     Returns (first_bad, bitmap):
       to_host=True : (global first bad round or NONE_U64, list of 64-bit words at global positions)
-      to_host=False: (1-element int64 device tensor, INT64_MAX = none; device words at global bit
-                     positions). Shards whose lengths are multiples of 64 (all but the last) are
-                     concatenated as is; otherwise the words are re-packed on the device.
+      to_host=False: (1-element int64 tensor, INT64_MAX = none; int64 words at global bit positions),
+                     on bitmap_words' device.
     """
     import torch
     import torch.distributed as dist
 
     dev = bitmap_words.device
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if counts is None:
+        c_t = torch.tensor([count], dtype=torch.int64)
+        all_counts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        if dist.get_backend(group) == "gloo":
+            dist.all_gather(all_counts, c_t, group=group)
+        else:
+            gathered = torch.empty(world, dtype=torch.int64, device=dev)
+            dist.all_gather_into_tensor(gathered, c_t.to(dev), group=group)
+            all_counts = gathered.cpu().split(1)
+        counts = [int(c) for c in all_counts]
+    counts = list(counts)
+    if len(counts) != world or counts[rank] != count:
+        raise ValueError(f"counts {counts} do not match world {world} / this shard's count {count}")
+    total = sum(counts)
+    tw = (total + 63) // 64
+    buf = torch.zeros(tw + world, dtype=torch.int64, device=dev)
+    place_words(buf, bitmap_words, count, sum(counts[:rank]))
     if isinstance(first_bad, int):
-        fb = torch.tensor([to_i64_first_bad(first_bad)], dtype=torch.int64, device=dev)
+        buf[tw + rank] = to_i64_first_bad(first_bad)
     else:
         fb = first_bad.reshape(1).to(torch.int64)
-        fb = torch.where(fb < 0, torch.full_like(fb, NONE_I64), fb)
-    dist.all_reduce(fb, op=dist.ReduceOp.MIN, group=group)
-    words = (count + 63) // 64
-    if not to_host and counts is not None and all(c % 64 == 0 for c in counts[:-1]) \
-            and len({(c + 63) // 64 for c in counts}) == 1:
-        # the bench path: every shard covers the same whole number of words
-        gathered = torch.empty(world * words, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(gathered, bitmap_words[:words].contiguous(), group=group)
-        return fb, gathered
-    if counts is None:
-        c_t = torch.tensor([count], dtype=torch.int64, device=dev)
-        all_counts = torch.empty(world, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(all_counts, c_t, group=group)
-        counts = [int(c) for c in all_counts.cpu().tolist()]
-    counts_l = list(counts)
-    wmax = max((c + 63) // 64 for c in counts_l)
-    padded = torch.zeros(wmax, dtype=torch.int64, device=dev)
-    padded[:words] = bitmap_words[:words]
-    gathered = torch.empty(world * wmax, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(gathered, padded, group=group)
+        buf[tw + rank:tw + rank + 1] = torch.where(fb < 0, torch.full_like(fb, NONE_I64), fb)
+    if dist.get_backend(group) == "gloo" and buf.device.type != "cpu":
+        host = buf.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        buf.copy_(host)
+    else:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    fb_all = buf[tw:].min().reshape(1)
     if not to_host:
-        return fb, repack_words(gathered, counts_l, wmax)
-    host_words = [w & NONE_U64 for w in gathered.cpu().tolist()]
-    return from_i64_first_bad(int(fb.item())), assemble_bitmap(host_words, counts_l, wmax)
+        return fb_all, buf[:tw]
+    return from_i64_first_bad(int(fb_all.item())), [w & NONE_U64 for w in buf[:tw].cpu().tolist()]
+
+
+def first_zero_bit(words, total: int):
+    """Index of the first 0 bit among the first ``total`` bits of an int64 word tensor, or None (a
+    check of the exchanged bitmap against the exchanged first bad round: for a history starting at
+    round 1 the first bad round is this index + 1)."""
+    import torch
+
+    nw = (total + 63) // 64
+    if nw == 0:
+        return None
+    w = words[:nw].clone()
+    if total % 64:
+        w[-1] |= -(1 << (total % 64))  # bits past the history count as accepted
+    bad = torch.nonzero(w != -1)
+    if bad.numel() == 0:
+        return None
+    q = int(bad[0, 0])
+    inv = (~int(w[q])) & NONE_U64
+    return 64 * q + ((inv & -inv).bit_length() - 1)
 
 
 def assemble_bitmap(words, counts, stride):
-    """Concatenate per-shard bitmaps (shard r's words at words[r*stride:]) at global bit offsets."""
+    """Host reference of the exchange's bit placement: per-shard bitmaps (shard r's words at
+    words[r*stride:]) concatenated at global bit offsets."""
     total = sum(counts)
     out = [0] * ((total + 63) // 64)
     pos = 0
@@ -153,35 +185,29 @@ def assemble_bitmap(words, counts, stride):
     return out
 
 
-def repack_words(gathered, counts, stride):
-    """Device form of assemble_bitmap: per-shard words (shard r at gathered[r*stride:]) -> one
-    bitmap at global bit offsets. Word-level bit-offset shifts with torch ops on the tensor's device:
-    shard r, starting at global bit pos = 64 q + s, ORs (w << s) into words q.. and the spill
-    (w >>> (64 - s)) into words q+1..; O(words) per shard, no per-bit temporaries (a 100M-round
-    bitmap is 1.56M words)."""
+def place_words(out, words, count: int, pos: int):
+    """OR the first ``count`` bits of ``words`` (int64 tensor, LSB first) into ``out`` (int64 tensor
+    on the same device) starting at global bit ``pos``: word-level shifts with torch ops on the
+    device, O(words), no per-bit temporaries (a 100M-round bitmap is 1.56M words)."""
     import torch
 
-    dev = gathered.device
-    total = int(sum(counts))
-    out = torch.zeros(max(1, (total + 63) // 64), dtype=torch.int64, device=dev)
-    pos = 0
-    for r, c in enumerate(counts):
-        nw = (c + 63) // 64
-        if nw == 0:
-            continue
-        w = gathered[r * stride: r * stride + nw].clone()
-        nb = c - 64 * (nw - 1)
-        if nb < 64:
-            w[-1] &= (1 << nb) - 1  # bits past the shard's last beacon
-        q, s = divmod(pos, 64)
-        out[q:q + nw] |= w << s if s else w
-        if s:
-            spill = (w >> (64 - s)) & ((1 << s) - 1)  # logical shift of the int64 words
-            hi = min(nw, out.numel() - q - 1)
-            if hi > 0:
-                out[q + 1:q + 1 + hi] |= spill[:hi]
-        pos += c
-    return out[:(total + 63) // 64]
+    nw = (count + 63) // 64
+    if nw == 0:
+        return out
+    w = words[:nw].to(out.device).clone()
+    nb = count - 64 * (nw - 1)
+    if nb < 64:
+        w[-1] &= (1 << nb) - 1  # bits past the shard's last beacon
+    q, s = divmod(pos, 64)
+    if not s:
+        out[q:q + nw] |= w
+        return out
+    out[q:q + nw] |= w << s
+    spill = (w >> (64 - s)) & ((1 << s) - 1)  # logical shift of the int64 words
+    hi = min(nw, out.numel() - q - 1)
+    if hi > 0:
+        out[q + 1:q + 1 + hi] |= spill[:hi]
+    return out
 
 
 def local_seeds(sl: SegmentedSlice, seg_seeds, gen_sigs):

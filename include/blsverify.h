@@ -234,7 +234,9 @@ int blsv_synchronize(blsv_ctx* ctx);
 /*
  * Latency-path cutover (see the latency contract above): calls with 1..lat_max items take the latency
  * path, larger ones the batch pipeline; 0 = batch pipeline only. The default is the BLSV_LAT_MAX
- * environment variable, else 2048 (where the two paths cross on MI355X). Returns the previous value.
+ * environment variable (a non-negative decimal integer; anything else is ignored with a warning on
+ * stderr), else 2048 (where the two paths cross on MI355X). Values above 2^20 (one pipeline chunk)
+ * are clamped to 2^20. Returns the previous value.
  */
 size_t blsv_set_lat_max(blsv_ctx* ctx, size_t lat_max);
 

@@ -35,10 +35,10 @@ int blsv_test_hash_to_g2(blsv_ctx* ctx, const uint8_t* msgs, const uint32_t* msg
 
 /*
  * Stage timing for bench.py's roofline: when enabled, every stage launch (0 hash, 1 decompress,
- * 2 miller, 3 final_exp, 4 finish) is bracketed by HIP events on its launch stream.
- * blsv_profile_read waits for the recorded events, writes per-stage summed milliseconds, launch
- * counts and items processed (arrays of nstages), clears the records and returns the number of
- * stages the engine defines (5).
+ * 2 miller, 3 final_exp, 4 finish, 5 lat = a whole batch on the latency path) is bracketed by HIP
+ * events on its launch stream. blsv_profile_read waits for the recorded events, writes per-stage
+ * summed milliseconds, launch counts and items processed (arrays of nstages), clears the records and
+ * returns the number of stages the engine defines (6).
  */
 int blsv_profile_enable(blsv_ctx* ctx, int on);
 int blsv_profile_read(blsv_ctx* ctx, double* ms, uint64_t* launches, uint64_t* items, int nstages);

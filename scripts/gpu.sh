@@ -1,0 +1,82 @@
+# One parameterised GPU-box runner (replaces the per-round scripts/gpu_r0*.sh).
+#
+#   gpurun -- bash scripts/gpu.sh TAG STEP [STEP ...]
+#
+# Output goes to gpurun_out/TAG/. Steps run in order; the first failing step ends the call (no GPU
+# step runs after a failure, a time limit or a fault). Steps:
+#   tests            pytest -m gpu (the whole GPU suite)
+#   tests:EXPR       pytest -m gpu -k EXPR
+#   smoke            __graft_entry__.smoke() (no torch in the process) + the plain-C ABI harness
+#   bench            default bench.py (configs[1], cpu_baseline)
+#   bench2           bench.py --gpus 2 --dist-backend gloo, weak and strong (two ranks on one GPU)
+#   prof             rocprofv3 --kernel-trace --stats of bench.py with BLSV_SERIAL_STAGES=1
+#   pmc              PMC passes: FETCH_SIZE, WRITE_SIZE, two SQ/GRBM sets (tools/pmc_sq.py)
+#   cabi             tools/cabi_smoke (latency contract from plain C)
+#   lat              tools/latency_bench.py (lone verify, fused round, crossover sweep)
+#   cfg              tools/config_bench.py (configs[2], configs[4], partials, drand.db)
+#   variant:NAME     GPU suite + bench on variants/libblsverify_NAME.so (scripts/build_variant.sh,
+#                    loaded through DRAND_AMD_LIB)
+#   vbench:NAME      bench only on that variant (same-box A/B against a plain `bench` step)
+set -o pipefail
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 2
+TAG=$1
+shift
+O=gpurun_out/$TAG
+mkdir -p "$O"
+PYT="python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread"
+B262="python3 -u bench.py --n 262144 --steps 1 --warmup 0 --cpu-per-worker 0"
+rc=0
+for step in "$@"; do
+  echo "[gpu.sh] $step $(date +%T)"
+  case "$step" in
+    tests) timeout -k 10 900 $PYT > "$O/pytest_gpu.log" 2>&1 || rc=12 ;;
+    tests:*) timeout -k 10 900 $PYT -k "${step#tests:}" > "$O/pytest_gpu_k.log" 2>&1 || rc=12 ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || rc=11 ;;
+    bench) timeout -k 10 400 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" || rc=13 ;;
+    bench2)
+      timeout -k 10 300 python -u bench.py --gpus 2 --dist-backend gloo --n 262144 --steps 2 --warmup 1 \
+        --cpu-per-worker 0 > "$O/bench2_weak.json" 2> "$O/bench2_weak.err" &&
+      timeout -k 10 300 python -u bench.py --gpus 2 --dist-backend gloo --total-rounds 524291 --steps 2 \
+        --warmup 1 --cpu-per-worker 0 > "$O/bench2_strong.json" 2> "$O/bench2_strong.err" || rc=14 ;;
+    prof)
+      BLSV_SERIAL_STAGES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" \
+        -o run -- python3 -u bench.py --steps 3 --warmup 1 --cpu-per-worker 0 > "$O/bench_serial_prof.json" \
+        2> "$O/prof.log" || rc=15 ;;
+    pmc)
+      PA="SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE"
+      PB="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT"
+      timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run -- $B262 \
+        > "$O/pmc_fetch.log" 2>&1 &&
+      timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o run -- $B262 \
+        > "$O/pmc_write.log" 2>&1 &&
+      timeout -s KILL 240 rocprofv3 --pmc $PA --output-format csv -d "$O/pmc_a" -o run -- $B262 > "$O/pmc_a.log" 2>&1 &&
+      timeout -s KILL 240 rocprofv3 --pmc $PB --output-format csv -d "$O/pmc_b" -o run -- $B262 > "$O/pmc_b.log" 2>&1 &&
+      python3 tools/pmc_sq.py "$O/pmc_sq.json" "$O/pmc_a/run_counter_collection.csv" \
+        "$O/pmc_b/run_counter_collection.csv" > /dev/null &&
+      python3 tools/pmc_traffic.py "$O/pmc_fetch/run_counter_collection.csv" \
+        "$O/pmc_write/run_counter_collection.csv" 262144 "$O/pmc_traffic.json" > /dev/null || rc=16 ;;
+    cabi) timeout -k 10 120 tools/cabi_smoke > "$O/cabi_smoke.txt" 2>&1 || rc=20 ;;
+    lat) timeout -k 10 300 python -u tools/latency_bench.py --reps 10 --out "$O/latency.json" > "$O/latency.log" 2>&1 || rc=21 ;;
+    cfg) timeout -k 10 600 python -u tools/config_bench.py > "$O/config_bench.json" 2> "$O/config_bench.log" || rc=22 ;;
+    variant:*)
+      V=${step#variant:}
+      L=variants/libblsverify_$V.so
+      if [ ! -f "$L" ]; then echo "no $L"; rc=30; else
+        DRAND_AMD_LIB=$L timeout -k 10 900 $PYT > "$O/pytest_gpu_$V.log" 2>&1 &&
+        DRAND_AMD_LIB=$L timeout -k 10 400 python -u bench.py --cpu-per-worker 0 > "$O/bench_$V.json" \
+          2> "$O/bench_$V.err" || rc=31
+      fi ;;
+    vbench:*)
+      V=${step#vbench:}
+      L=variants/libblsverify_$V.so
+      if [ ! -f "$L" ]; then echo "no $L"; rc=30; else
+        DRAND_AMD_LIB=$L timeout -k 10 400 python -u bench.py --cpu-per-worker 0 > "$O/bench_$V.json" \
+          2> "$O/bench_$V.err" || rc=31
+      fi ;;
+    *) echo "unknown step $step"; rc=2 ;;
+  esac
+  [ $rc -eq 0 ] || { echo "[gpu.sh] step $step failed rc=$rc"; exit $rc; }
+done
+echo "[gpu.sh] done $(date +%T)"

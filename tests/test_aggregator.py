@@ -149,6 +149,28 @@ def test_aggregator_cpu(small_group):
     assert sum(1 for c in eng.calls if c[0] == "aggregate_round") == 7
 
 
+def _short_share_round(engine, g):
+    """A V1 share and a V2 share of the wrong length in one round cache. They cannot parse, so
+    VerifyPartial rejects them and kyber's Recover skips them, but they still count in
+    roundCache.Len()/LenV2() (cache.go:148-161): with LenV2() = t and only t - 1 valid V2 shares the
+    V2 Recover runs and fails, which blocks the beacon (chain.go:153-160)."""
+    t, n = g["t"], g["n"]
+    prev = b"\x11" * 32
+    pk = _packets(g, 1, prev, [0, 1, 2, 3])
+    p1 = [pk[0].partial_sig[:50]] + [p.partial_sig for p in pk[1:]]
+    p2 = [pk[0].partial_sig_v2, pk[1].partial_sig_v2[:97], pk[2].partial_sig_v2]
+    return engine.aggregate_round(C.message(1, prev), p1, C.message_v2(1), p2, t, n)
+
+
+def test_short_shares_count_toward_the_gate_cpu(small_group):
+    from tests.support.oracle_engine import OracleEngine
+    eng = OracleEngine()
+    eng.set_group(small_group["commits"], small_group["n"])
+    st, ok1, ok2, sig1, sig2, _ = _short_share_round(eng, small_group)
+    assert st == C.AGG_V2_RECOVER_FAIL and ok1 == [False, True, True, True] and ok2 == [True, False, True]
+    assert sig1 == small_group["sign"](small_group["coeffs"][0], C.message(1, b"\x11" * 32)) and sig2 is None
+
+
 class _FakeV2Invalid:
     """A V2 VerifyRecovered failure only logs (chain.go:162-164): the beacon still carries the V2
     signature. Unreachable with consistent shares (Recover of valid shares always verifies), so the
@@ -174,6 +196,20 @@ def test_v2_verify_failure_only_logs():
 def test_aggregator_gpu(engine, small_group):
     stored = _scenarios(engine, small_group)
     assert [b.round for b in stored] == [1, 2, 3, 4]
+
+
+@pytest.mark.gpu
+def test_short_shares_count_toward_the_gate_gpu(engine, small_group):
+    """Same round through blsv_aggregate_round: status, ok positions and sig1 equal the oracle
+    engine's (a short share must not shrink k2 and skip the V2 Recover)."""
+    from tests.support.oracle_engine import OracleEngine
+    ref = OracleEngine()
+    ref.set_group(small_group["commits"], small_group["n"])
+    engine.set_group(small_group["commits"], small_group["n"])
+    got = _short_share_round(engine, small_group)
+    want = _short_share_round(ref, small_group)
+    assert got[:4] == want[:4] and got[4] is None
+    assert got[0] == C.AGG_V2_RECOVER_FAIL
 
 
 @pytest.mark.gpu

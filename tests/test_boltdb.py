@@ -191,7 +191,7 @@ def _sharded_worker(rank, world, port, path, pk, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_verify_store_sharded_gloo(tmp_path, chain, world):
-    """Row (e) over row (f): ranks split the stored entries, combine with MIN + all-gather (gloo)."""
+    """Row (e) over row (f): ranks split the stored entries, combine with one SUM all-reduce (gloo)."""
     import multiprocessing as mp
     import socket
     pk, _, bs = chain

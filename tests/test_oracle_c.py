@@ -91,3 +91,19 @@ def test_threshold_golden(C, golden):
         assert g.recover(msg, sub[:-1] + [sub[0]], th["t"], th["n"]) is None  # a duplicate counts, collapses
     finally:
         g.close()
+
+
+def test_chain2049_fixture_is_the_golden_chain(golden):
+    """tests/golden/chain2049.bin (make_chain_fixture.py) continues the golden chained history: its
+    first rounds are the golden beacons byte for byte, and the C oracle accepts samples further on."""
+    from oracle import c_oracle
+
+    c_oracle.load()
+    with open(os.path.join(os.path.dirname(__file__), "golden", "chain2049.bin"), "rb") as f:
+        raw = f.read()
+    assert len(raw) == 2049 * 96
+    ch = golden["chained"]
+    assert [raw[i * 96:(i + 1) * 96].hex() for i in range(len(ch["beacons"]))] == [b["sig"] for b in ch["beacons"]]
+    pk = bytes.fromhex(ch["pk"])
+    for lo in (1999, 2047):
+        assert c_oracle.verify_chained(pk, lo + 1, raw[(lo - 1) * 96:lo * 96], raw[lo * 96:(lo + 2) * 96]) == [0, 0]

@@ -1,6 +1,7 @@
 """Multi-GPU sharding logic on the CPU: contiguous round ranges, the one-signature
-halo, and the exchange step (MIN of first bad round + bitmap all-gather) over torch.distributed with
-the gloo backend at world_size 2 and 3 -- the same code bench.py runs over RCCL."""
+halo, and the exchange step (ONE SUM all-reduce of the global-position bitmap plus per-rank first-bad
+slots) over torch.distributed with the gloo backend at world_size 2 and 3 -- the same code bench.py
+runs over RCCL."""
 import os
 import random
 import socket
@@ -61,23 +62,35 @@ def test_assemble_bitmap_unaligned():
 
 @pytest.mark.parametrize("counts", [[70, 1, 129, 64], [12_500_000 % 4099 + 1, 4099, 63, 65, 1, 0, 200],
                                     [64, 64, 64], [1], [127, 129, 1000, 3]])
-def test_repack_words_matches_assemble(counts):
-    """The word-shift device repack (bench.py's unaligned configs[3] shards) equals the host
-    assembler bit for bit, garbage past each shard masked, sign bit (bit 63) included."""
+def test_place_words_matches_assemble(counts):
+    """The word-shift placement every rank does before the one all-reduce: each shard's words ORed
+    in at its global bit offset (garbage past each shard masked, sign bit 63 included) and summed over
+    the shards equals the host assembler bit for bit -- SUM of disjoint bits is OR."""
     rng = random.Random(sum(counts))
     bits = [rng.random() < 0.6 for _ in range(sum(counts))]
     stride = max(1, max((c + 63) // 64 for c in counts))
     words, pos = [], 0
+    total_words = (sum(counts) + 63) // 64
+    acc = torch.zeros(max(1, total_words), dtype=torch.int64)
     for c in counts:
         w = _bits_to_words(bits[pos:pos + c])
         w += [0xFFFFFFFFFFFFFFFF] * (stride - len(w))
         if w and c % 64:
             w[(c - 1) // 64] |= ~((1 << (c % 64)) - 1) & 0xFFFFFFFFFFFFFFFF  # garbage in the last word
         words += w
+        part = torch.zeros(max(1, total_words), dtype=torch.int64)
+        shard.place_words(part, _to_i64(w[:stride]), c, pos)
+        acc += part  # what the SUM all-reduce does
         pos += c
-    got = shard.repack_words(_to_i64(words), counts, stride)
-    assert [x & shard.NONE_U64 for x in got.tolist()] == shard.assemble_bitmap(words, counts, stride) \
-        == _bits_to_words(bits)
+    got = [x & shard.NONE_U64 for x in acc.tolist()][:total_words]
+    assert got == shard.assemble_bitmap(words, counts, stride) == _bits_to_words(bits)
+
+
+def test_first_zero_bit():
+    for total, bad in [(1, None), (64, 63), (65, 64), (130, 0), (200, 127), (1000, None), (129, 128)]:
+        bits = [i != bad for i in range(total)]
+        w = _to_i64(_bits_to_words(bits) + [0])  # a trailing zero word past the history is ignored
+        assert shard.first_zero_bit(w, total) == bad
 
 
 def _free_port():
@@ -100,11 +113,22 @@ def _worker(rank, world, port, n, bad, q):
         local_bad = [sh.first_round + i for i, b in enumerate(bits) if not b]
         fb = min(local_bad) if local_bad else shard.NONE_U64
         words = _to_i64(_bits_to_words(bits)) if bits else torch.zeros(0, dtype=torch.int64)
+        calls = []
+        real = {k: getattr(dist, k) for k in ("all_reduce", "all_gather", "all_gather_into_tensor", "broadcast")}
+        counts = [shard.shard_range(n, world, r).count for r in range(world)]
+        try:  # count the collectives one exchange issues (counts known, as in bench.py)
+            for k, f in real.items():
+                setattr(dist, k, lambda *a, _k=k, _f=f, **kw: (calls.append(_k), _f(*a, **kw))[1])
+            d_fb0, _ = shard.combine(fb, words, sh.count, to_host=False, counts=counts)
+        finally:
+            for k, f in real.items():
+                setattr(dist, k, f)
         g_fb, g_words = shard.combine(fb, words, sh.count)
         # device form (the bench path), as the kernels write it: UINT64_MAX = -1 in an int64 tensor
         fb_t = torch.tensor([-1 if fb == shard.NONE_U64 else fb], dtype=torch.int64)
         d_fb, d_words = shard.combine(fb_t, words, sh.count, to_host=False)
-        q.put((rank, g_fb, g_words, int(d_fb.item()), [w & shard.NONE_U64 for w in d_words.tolist()]))
+        q.put((rank, g_fb, g_words, int(d_fb.item()), [w & shard.NONE_U64 for w in d_words.tolist()], calls,
+               shard.first_zero_bit(d_words, n)))
     finally:
         dist.destroy_process_group()
 
@@ -124,13 +148,13 @@ def test_combine_gloo(world, n, bad):
         assert p.exitcode == 0
     want_words = _bits_to_words([i not in bad for i in range(n)])
     want_fb = min(bad) + 1 if bad else shard.NONE_U64  # ROUND = index + 1
-    aligned = all(shard.shard_range(n, world, r).count % 64 == 0 for r in range(world - 1))
-    for rank, g_fb, g_words, d_fb, d_words in res:
+    for rank, g_fb, g_words, d_fb, d_words, calls, fz in res:
+        assert calls == ["all_reduce"]  # one collective per exchange (north_star: a single all-reduce)
         assert g_fb == want_fb
         assert g_words == want_words
-        assert d_fb == (shard.NONE_I64 if not bad else want_fb)  # the regression the MIN mapping fixes
-        if aligned:
-            assert d_words[:len(want_words)] == want_words
+        assert d_fb == (shard.NONE_I64 if not bad else want_fb)  # UINT64_MAX (-1) must not win the MIN
+        assert d_words == want_words
+        assert fz == (min(bad) if bad else None)  # the bitmap agrees with the exchanged first bad round
 
 
 # --------------------------------------------------------------------------------------------------
@@ -208,7 +232,7 @@ def test_split_real_history_matches_single_rank(real_history, world):
     for rank, g_fb, g_words, d_fb, d_words in res:
         assert g_fb == 75 and d_fb == 75  # ROUND of index 74
         assert g_words == want_words
-        assert d_words == want_words  # device re-pack of unaligned shards
+        assert d_words == want_words  # device placement of unaligned shards
 
 
 def test_segmented_slice_seed_rule(golden):
