@@ -149,14 +149,7 @@ DI bool jac_eq(const jac<F>& p, const jac<F>& q) {
 // G2 doubling (dbl-2009-l, as jac_dbl) with the Fp2 products expanded in place: the [x] chains of
 // the G2 cofactor clearing and subgroup check run their 63 doublings call-free, so the register
 // allocator sees the whole step instead of the AMDGPU call ABI's caller/callee-saved split.
-#ifndef BLS_G2_DBL_FENCE
-#define BLS_G2_DBL_FENCE 0
-#endif
-#if BLS_G2_DBL_FENCE
-#define G2_DBL_FENCE() BLS_SCHED_FENCE()
-#else
 #define G2_DBL_FENCE() ((void)0)
-#endif
 DI g2j g2_dbl_inl(const g2j& p) {
   const fp2 Z3 = fp2_dbl(fp2_mul_inl(p.y, p.z));
   G2_DBL_FENCE();
@@ -176,12 +169,9 @@ DI g2j g2_dbl_inl(const g2j& p) {
   return {X3, Y3, Z3};
 }
 
-#ifndef BLS_G2_DBL_INL
-#define BLS_G2_DBL_INL 1
-#endif
 template <typename F>
 DI jac<F> jac_dbl_chain(const jac<F>& p) {
-  if constexpr (BLS_G2_DBL_INL && sizeof(F) == sizeof(fp2)) {
+  if constexpr (sizeof(F) == sizeof(fp2)) {
     return g2_dbl_inl(p);
   } else {
     return jac_dbl(p);
@@ -310,157 +300,7 @@ DI g2j g2_mul_x_abs_inl(const g2j& p, Base base) {
   return acc;
 }
 
-#ifndef BLS_G2_ACC_LDS
-#define BLS_G2_ACC_LDS 0
-#endif
-#if BLS_G2_ACC_LDS
-// The [x] chains with the accumulator's X and Y parked in LDS (48 words per lane, word-major: 12 KB
-// per one-wave workgroup, beside the 6 KB of g_fp2_arg: 8 workgroups per CU at 2 waves/SIMD) and Z
-// in registers; each coordinate is written back after the last use of its old value, and the base
-// point's coordinates are re-read at each use. Same operations on the same values as g2_dbl_inl /
-// g2_add_inl / g2_madd_inl.
-#ifdef BLS_HOST
-static uint32_t g_g2_acc[48 * BLS_LANES];
-#else
-static __shared__ uint32_t g_g2_acc[48 * BLS_LANES];
-#endif
-struct g2acc_lds {
-  uint32_t* base;
-  fp2* z;
-  DI fp2 get(int c) const {
-    if (c == 2) return *z;
-    fp2 v;
-#pragma unroll
-    for (int w = 0; w < 12; w++) {
-      v.c0.l[w] = base[(24 * c + w) * BLS_LANES];
-      v.c1.l[w] = base[(24 * c + 12 + w) * BLS_LANES];
-    }
-    return v;
-  }
-  DI void set(int c, const fp2& v) const {
-    if (c == 2) {
-      *z = v;
-      return;
-    }
-#pragma unroll
-    for (int w = 0; w < 12; w++) {
-      base[(24 * c + w) * BLS_LANES] = v.c0.l[w];
-      base[(24 * c + 12 + w) * BLS_LANES] = v.c1.l[w];
-    }
-  }
-};
-
-template <typename TS>
-DI void g2_dbl_ts(const TS& t) {
-  t.set(2, fp2_dbl(fp2_mul_inl(t.get(1), t.get(2))));  // Z3 (Z has had its last use)
-  G2_DBL_FENCE();
-  const fp2 A = fp2_sqr_inl(t.get(0));
-  G2_DBL_FENCE();
-  const fp2 B = fp2_sqr_inl(t.get(1));
-  G2_DBL_FENCE();
-  const fp2 C = fp2_sqr_inl(B);
-  G2_DBL_FENCE();
-  const fp2 D = fp2_dbl(fp2_sub(fp2_sub(fp2_sqr_inl(fp2_add(t.get(0), B)), A), C));
-  G2_DBL_FENCE();
-  const fp2 E = fp2_add(fp2_dbl(A), A);
-  const fp2 X3 = fp2_sub(fp2_sqr_inl(E), fp2_dbl(D));
-  t.set(0, X3);
-  G2_DBL_FENCE();
-  const fp2 C8 = fp2_dbl(fp2_dbl(fp2_dbl(C)));
-  t.set(1, fp2_sub(fp2_mul_inl(E, fp2_sub(D, X3)), C8));
-}
-
-// acc += base() (AFF: base() affine, never infinity -> madd-2007-bl; else add-2007-bl). A lane whose
-// addition is exceptional (acc or base at infinity, acc == +-base) writes the called formulas'
-// result at once and skips the generic writes.
-template <bool AFF, typename TS, typename Base>
-DI void g2_add_ts(const TS& t, Base base) {
-  const fp2 Z1Z1 = fp2_sqr_inl(t.get(2));
-  BLS_SCHED_FENCE();
-  fp2 U1, S1, H, r, Z2Z2;
-  if constexpr (AFF) {
-    U1 = t.get(0);
-    S1 = t.get(1);
-    const fp2 U2 = fp2_mul_inl(base().x, Z1Z1);
-    BLS_SCHED_FENCE();
-    const fp2 S2 = fp2_mul_inl(fp2_mul_inl(base().y, t.get(2)), Z1Z1);
-    H = fp2_sub(U2, U1);
-    r = fp2_dbl(fp2_sub(S2, S1));
-  } else {
-    Z2Z2 = fp2_sqr_inl(base().z);
-    BLS_SCHED_FENCE();
-    U1 = fp2_mul_inl(t.get(0), Z2Z2);
-    BLS_SCHED_FENCE();
-    S1 = fp2_mul_inl(fp2_mul_inl(t.get(1), base().z), Z2Z2);
-    BLS_SCHED_FENCE();
-    const fp2 U2 = fp2_mul_inl(base().x, Z1Z1);
-    BLS_SCHED_FENCE();
-    const fp2 S2 = fp2_mul_inl(fp2_mul_inl(base().y, t.get(2)), Z1Z1);
-    H = fp2_sub(U2, U1);
-    r = fp2_dbl(fp2_sub(S2, S1));
-  }
-  BLS_SCHED_FENCE();
-  const bool pinf = fp2_is_zero(t.get(2)), h0 = fp2_is_zero(H);
-  bool exc = pinf | h0;
-  if constexpr (!AFF) exc |= fp2_is_zero(base().z);
-  if (exc) {  // per lane, rare
-    const g2j p = {t.get(0), t.get(1), t.get(2)};
-    g2j o;
-    if constexpr (AFF) {
-      o = pinf ? jac_from_aff(base()) : (fp2_is_zero(r) ? jac_dbl(p) : jac_infinity<fp2>());
-    } else {
-      const g2j q = base();
-      o = pinf ? q : (jac_is_inf(q) ? p : (fp2_is_zero(r) ? jac_dbl(p) : jac_infinity<fp2>()));
-    }
-    t.set(0, o.x);
-    t.set(1, o.y);
-    t.set(2, o.z);
-  }
-  fp2 I, HH;
-  if constexpr (AFF) {
-    HH = fp2_sqr_inl(H);
-    I = fp2_dbl(fp2_dbl(HH));
-  } else {
-    I = fp2_sqr_inl(fp2_dbl(H));
-  }
-  BLS_SCHED_FENCE();
-  const fp2 J = fp2_mul_inl(H, I);
-  BLS_SCHED_FENCE();
-  const fp2 V = fp2_mul_inl(U1, I);
-  BLS_SCHED_FENCE();
-  const fp2 X3 = fp2_sub(fp2_sub(fp2_sqr_inl(r), J), fp2_dbl(V));
-  BLS_SCHED_FENCE();
-  const fp2 Y3 = fp2_sub(fp2_mul_inl(r, fp2_sub(V, X3)), fp2_dbl(fp2_mul_inl(S1, J)));
-  BLS_SCHED_FENCE();
-  fp2 Z3;
-  if constexpr (AFF)
-    Z3 = fp2_sub(fp2_sub(fp2_sqr_inl(fp2_add(t.get(2), H)), Z1Z1), HH);
-  else
-    Z3 = fp2_mul_inl(fp2_sub(fp2_sub(fp2_sqr_inl(fp2_add(t.get(2), base().z)), Z1Z1), Z2Z2), H);
-  if (!exc) {
-    t.set(0, X3);
-    t.set(1, Y3);
-    t.set(2, Z3);
-  }
-}
-
-template <bool AFF, typename Base>
-DI g2j g2_mul_x_abs_lds(const g2j& p, Base base) {
-  fp2 z = p.z;
-  const g2acc_lds t{g_g2_acc + bls_lane(), &z};
-  t.set(0, p.x);
-  t.set(1, p.y);
-#pragma unroll 1
-  for (int i = 62; i >= 0; i--) {
-    g2_dbl_ts(t);
-    if ((BLS_X_ABS >> i) & 1ull) g2_add_ts<AFF>(t, base);
-  }
-  return {t.get(0), t.get(1), z};
-}
-#define G2_MUL_X_ABS_CHAIN g2_mul_x_abs_lds
-#else
 #define G2_MUL_X_ABS_CHAIN g2_mul_x_abs_inl
-#endif
 
 // g2_in_subgroup for an affine point re-read by `reload` (never infinity: the caller screens it)
 template <typename Reload>

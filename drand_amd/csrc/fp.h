@@ -468,24 +468,6 @@ DI u24 fp2_mul_body(const u24& a, const u12& b0, const u12& b1) {
 // against NEG28_16P, whose limbs are at least any operand limb). A squaring operand is at most ONE
 // lazy sum (< 4p; every fp2_sqr* call site squares a reduced value or one fp2_add_lazy): the values
 // stay below 20p, the column sums below 2^62.6 and the result below 2p (operand contract above).
-#ifndef BLS_FP2_SQR28
-#define BLS_FP2_SQR28 1
-#endif
-#if !BLS_FP2_SQR28
-// the r02 form (A/B): the sums as 12-word carry chains, then split
-DI u24 fp2_sqr_body(const u24& a) {
-  const u12 a0 = u24_lo(a), a1 = u24_hi(a);
-  uint32_t x[14], y[14];
-  fp_split28(fp_add_raw_u12(a0, a1), x);
-  fp_split28(fp_add_raw_u12(a0, fp_4p_minus_u12(a1)), y);
-  const u12 c0 = fp_mont_dot<false>(x, y, x, y);
-  BLS_SCHED_FENCE();
-  fp_split28(fp_add_raw_u12(a0, a0), x);
-  fp_split28(a1, y);
-  const u12 c1 = fp_mont_dot<false>(x, y, x, y);
-  return u24_of(c0, c1);
-}
-#else
 DI u24 fp2_sqr_body(const u24& a) {
   uint32_t s0[14], s1[14], x[14], y[14];
   fp_split28(u24_lo(a), s0);
@@ -502,7 +484,6 @@ DI u24 fp2_sqr_body(const u24& a) {
   const u12 c1 = fp_mont_dot<false>(x, s1, x, s1);
   return u24_of(c0, c1);
 }
-#endif
 
 // The called forms: b of fp2_mul_u24 comes from fp2_arg_store (LDS), one copy of each body per
 // code object. The _inl forms (tower.h fp2_mul_inl / fp2_sqr_inl) expand the bodies in place for
@@ -597,13 +578,6 @@ DI fp fp_pow_words(const fp& a, const uint32_t (&e)[NW]) {
 NOINL u12 fp_pow_p_minus_2(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_2)); }
 NOINL u12 fp_pow_sqrt(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_PLUS_1_DIV_4)); }
 NOINL u12 fp_pow_legendre(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_1_DIV_2)); }
-#ifndef BLS_SQRT_W4
-#define BLS_SQRT_W4 1
-#endif
-#ifndef BLS_SQRT_SQR_INL
-#define BLS_SQRT_SQR_INL 1
-#endif
-#if BLS_SQRT_W4
 // Montgomery square / product with the running value kept split in radix 2^28 (14 limbs < 2^28, the
 // output form of the column loops): an exponentiation's chain of squares skips fp_split28 /
 // fp_join28 at every step
@@ -655,7 +629,6 @@ NOINL u12 fp_pow_p_minus_3_div_4(u12 a12) {
     const int ent = EXP_SQRT_W4[e], nsq = ent >> 8, d = (ent & 255) >> 1;
 #pragma unroll 1
     for (int k = 0; k < nsq; k++) {
-#if BLS_SQRT_SQR_INL
       BLS_COUNT_MUL();
       uint32_t x[14], tt[14];
 #pragma unroll
@@ -663,9 +636,6 @@ NOINL u12 fp_pow_p_minus_3_div_4(u12 a12) {
       fp_sqr28_t(x, tt);
 #pragma unroll
       for (int q = 0; q < 14; q++) r[q] = tt[q];
-#else
-      r = fp_sqr_r28(r);
-#endif
     }
     fp t = tab[0];
 #pragma unroll
@@ -679,9 +649,6 @@ NOINL u12 fp_pow_p_minus_3_div_4(u12 a12) {
   for (int k = 0; k < 14; k++) t[k] = r[k];
   return fp_join28(t);
 }
-#else
-NOINL u12 fp_pow_p_minus_3_div_4(u12 a) { return fp_to_u12(fp_pow_words<12>(fp_from_u12(a), EXP_P_MINUS_3_DIV_4)); }
-#endif
 
 // w = a^((p-3)/4): t = w*a satisfies t^2 = a (a a residue or 0) or t^2 = -a (non-residue), and
 // 1/t = w or -w respectively: a square root AND its inverse from one exponentiation.
@@ -857,11 +824,7 @@ NOINL u12 fp_inv_bingcd(u12 yin) {
   return r;
 }
 
-#ifndef BLS_INV_POW
 DI fp fp_inv(const fp& a) { return fp_from_u12(fp_inv_bingcd(fp_to_u12(a))); }  // 0 -> 0
-#else
-DI fp fp_inv(const fp& a) { return fp_from_u12(fp_pow_p_minus_2(fp_to_u12(a))); }  // 0 -> 0
-#endif
 
 // sqrt candidate a^((p+1)/4); caller checks the square
 DI fp fp_sqrt_cand(const fp& a) { return fp_from_u12(fp_pow_sqrt(fp_to_u12(a))); }

@@ -7,11 +7,8 @@ namespace blsk {
 // Two kernels: decoding (flag, infinity form, x < p, the Fp2 square root -- two Fp exponentiations with
 // a small live state, run at high occupancy) and the psi subgroup check ([x] chain on a Jacobian point:
 // many short calls). The reject order is kilic's: the subgroup check only runs on decoded points.
-#ifndef BLS_G2_CHAIN_INL
-#define BLS_G2_CHAIN_INL 1
-#endif
 #ifndef BLS_WPE_SUBGROUP
-#define BLS_WPE_SUBGROUP (BLS_G2_CHAIN_INL ? 2 : 1)
+#define BLS_WPE_SUBGROUP 2
 #endif
 
 BLS_KERNEL(BLS_WPE_DECOMP) k_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, size_t base,
@@ -38,17 +35,12 @@ BLS_KERNEL(BLS_WPE_DECOMP) k_decompress_g2(const uint8_t* sigs, size_t stride, s
 BLS_KERNEL(BLS_WPE_SUBGROUP) k_subgroup_g2(uint32_t* S, uint8_t* s_inf, uint8_t* cls, size_t cnt) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt || cls[i] != REJ_OK || s_inf[i]) return;
-#if BLS_G2_CHAIN_INL
   // the point is re-read at its uses (psi, the 5 additions) instead of living across the chain
   const bool in = g2_in_subgroup_aff_reload([&]() {
     size_t j = i;
     asm volatile("" : "+v"(j));
     return g2a{ld_fp2(S, cnt, j, 0), ld_fp2(S, cnt, j, 2)};
   });
-#else
-  const g2a a = {ld_fp2(S, cnt, i, 0), ld_fp2(S, cnt, i, 2)};
-  const bool in = g2_in_subgroup(jac_from_aff(a));
-#endif
   if (!in) {
     st_fp2(S, cnt, i, 0, fp2_zero());
     st_fp2(S, cnt, i, 2, fp2_zero());

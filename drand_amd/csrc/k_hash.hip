@@ -36,11 +36,8 @@ DI void store_jac(uint32_t* Q, size_t cnt, size_t i, int slot, const g2j& p) {
 #ifndef BLS_WPE_HASH_A
 #define BLS_WPE_HASH_A 4
 #endif
-#ifndef BLS_G2_CHAIN_INL
-#define BLS_G2_CHAIN_INL 1
-#endif
 #ifndef BLS_WPE_HASH_B
-#define BLS_WPE_HASH_B (BLS_G2_CHAIN_INL ? 2 : 1)
+#define BLS_WPE_HASH_B 2
 #endif
 #ifndef BLS_WPE_HASH_C
 #define BLS_WPE_HASH_C 4
@@ -131,13 +128,9 @@ BLS_KERNEL(BLS_WPE_HASH_B) k_hash_cofactor(uint32_t* Q, size_t cnt) {
     asm volatile("" : "+v"(j));  // re-read at each use, never kept live across the [x] chains
     return load_jac(Q, cnt, j, slot);
   };
-#if BLS_G2_CHAIN_INL
   // P in slots 0..5; the second chain's base A parks in slots 6..11 (q1 is dead by then)
   const g2j r = g2_clear_cofactor_inl([&]() { return at(0); }, [&](const g2j& a) { store_jac(Q, cnt, i, 6, a); },
                                       [&]() { return at(6); });
-#else
-  const g2j r = g2_clear_cofactor_reload([&]() { return at(0); });
-#endif
   store_jac(Q, cnt, i, 6, r);
 }
 

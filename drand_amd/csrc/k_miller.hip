@@ -16,10 +16,6 @@ DI int line_slot(int step, int k) { return (step * 2 + k) * 6; }
 // The two pairs run in separate workgroups (k = blockIdx.x & 1: the pair of the whole wave), so a
 // beacon's two line chains run side by side: half the latency of one lane walking both, twice the
 // waves (a finer tail), and every store still one 256-byte access per wave.
-#ifndef BLS_LINES_T_LDS
-#define BLS_LINES_T_LDS 1
-#endif
-#if BLS_LINES_INL == 2 && BLS_LINES_T_LDS
 static __shared__ uint32_t g_ml_T[72 * BLS_LANES];
 // T = (X, Y, Z) in LDS, word w of coordinate c at [(24 c + w) * 64 + lane]: conflict-free dword access
 struct g2proj_lds {
@@ -41,7 +37,6 @@ struct g2proj_lds {
     }
   }
 };
-#endif
 
 BLS_KERNEL(BLS_WPE_LINES)
 k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
@@ -68,7 +63,6 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
       st_fp2(LN, sub, i, s + 2, o.a1);
       st_fp2(LN, sub, i, s + 4, o.a4);
     };
-#if BLS_LINES_INL == 2
     // call-free steps (pairing.h miller_dbl_step_inl): P, Q and the lines never live across a call
     auto pcoord = [&](int c) {
       size_t o = (size_t)kk * G1_WORDS + 12 * c;
@@ -87,7 +81,6 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
     auto put = [&](int c, const fp2& v) { st_fp2(LN, sub, i, line_slot(step, k) + 2 * c, v); };
     auto xp = [&]() { return pcoord(0); };
     auto yp = [&]() { return pcoord(1); };
-#if BLS_LINES_T_LDS
     // T parks in LDS (72 words per lane, word-major: 18 KB per one-wave workgroup, 8 per CU at 2
     // waves/SIMD), read at each use and written back coordinate by coordinate
     const g2proj_lds T{g_ml_T + threadIdx.x};
@@ -97,14 +90,6 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
       T.set(1, Q0.y);
       T.set(2, fp2_one());
     }
-#else
-    g2proj Tr;
-    {
-      const g2a Q0 = load_q();
-      Tr = {Q0.x, Q0.y, fp2_one()};
-    }
-    const g2proj_reg T{Tr};
-#endif
 #pragma unroll 1
     for (int b = 62; b >= 0; b--) {
       miller_dbl_step_ts(T, put, xp, yp);
@@ -114,27 +99,9 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
         step++;
       }
     }
-#else
-    g1a P;
-    if (k == 0) {
-#pragma unroll
-      for (int w = 0; w < 12; w++) {
-        P.x.l[w] = pk_tab[(size_t)kk * G1_WORDS + w];
-        P.y.l[w] = pk_tab[(size_t)kk * G1_WORDS + 12 + w];
-      }
-    } else {
-      P.x = fp_load_const(G1_GEN_X);
-      P.y = fp_load_const(G1_GEN_NEG_Y);
-    }
-    miller_lines(P, load_q, emit);
-#endif
   }
 }
 
-#ifndef BLS_MF_LDS
-#define BLS_MF_LDS 1
-#endif
-#if BLS_MF_LDS
 // The line-pair product L (5 Fp2: c0.c0, c0.c1, c0.c2, c1.c1, c1.c2) of the current step parks in LDS
 // (one 120-word column per lane: 30 KB per one-wave workgroup, 4 per CU with g_fp2_arg) and is read
 // back at each use, so f (144 words) and the partial products are all that stay in registers.
@@ -185,7 +152,6 @@ DI fp12 fp12_mul_by_line_pair_lds(const fp12& f) {
                          t1);
   return {fp6_add(t0, fp6_mul_v(t1)), c1};
 }
-#endif
 
 BLS_KERNEL(BLS_WPE_MILLER_F) k_miller_f(const uint32_t* LN, const uint8_t* cls, size_t cnt, size_t base,
                                                   size_t m, size_t sub, uint32_t* F) {
@@ -197,7 +163,6 @@ BLS_KERNEL(BLS_WPE_MILLER_F) k_miller_f(const uint32_t* LN, const uint8_t* cls, 
     const int s = line_slot(step, k);
     return line{ld_fp2(LN, sub, i, s + 0), ld_fp2(LN, sub, i, s + 2), ld_fp2(LN, sub, i, s + 4)};
   };
-#if BLS_MF_LDS
   // miller_f_from_lines (pairing.h) with the line-pair product parked in LDS
   fp12 f = fp12_one();
   int step = 0;
@@ -225,9 +190,6 @@ BLS_KERNEL(BLS_WPE_MILLER_F) k_miller_f(const uint32_t* LN, const uint8_t* cls, 
     }
   }
   st_fp12(F, cnt, g, fp12_conj(f));
-#else
-  st_fp12(F, cnt, g, miller_f_from_lines(load));
-#endif
 }
 
 // ------------------------------------------------------------------ 3-lane f pass (tri.h)

@@ -31,14 +31,7 @@ static inline unsigned grid_for(size_t n) { return (unsigned)((n + TPB - 1) / TP
 #define BLS_WPE_FEXP 1
 #endif
 // amdgpu_waves_per_eu(n) asks for AT LEAST n waves/SIMD and the compiler may settle for fewer (it
-// gives the 4-wave exponentiation kernels 145 VGPRs = 3 waves); BLS_WPE_EXACT=1 pins min = max = n.
-#ifndef BLS_WPE_EXACT
-#define BLS_WPE_EXACT 0
-#endif
-#if BLS_WPE_EXACT
-#define BLS_KERNEL(wpe) __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(wpe, wpe)))
-#else
+// gives the 4-wave exponentiation kernels 145 VGPRs = 3 waves); min = max = n measured no better.
 #define BLS_KERNEL(wpe) __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(wpe)))
-#endif
 
 }  // namespace blsk

@@ -55,9 +55,8 @@ void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t
 constexpr size_t TRI_PARK_WORDS(size_t items) { return 48 * 64 * ((items + 20) / 21); }
 // F is clobbered; W = 3 * cnt * F_WORDS words of staging; out (optional, test hook): the
 // exponentiated values (SoA, cnt * F_WORDS words)
-// park: FEXP_PARK_WORDS(cnt) words of scratch: the six kept squares of the compressed chain
-// (Fp12 slots), then the park of the 3-lane products
-constexpr size_t FEXP_PARK_WORDS(size_t items) { return 6 * items * F_WORDS + TRI_PARK_WORDS(items); }
+// park: FEXP_PARK_WORDS(cnt) words of scratch for the 3-lane products' parked partial results
+constexpr size_t FEXP_PARK_WORDS(size_t items) { return TRI_PARK_WORDS(items); }
 void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st, uint32_t* park,
                       uint32_t* out = nullptr);
 // bitmap bit (base+i) = (cls[i] == 0); bitmap must cover whole 64-bit words;

@@ -49,43 +49,12 @@ DI void miller_dbl_step(g2proj& t, fp2& l00, fp2& l01, fp2& l11, const fp& xp, c
   t.z = mul(B, H);
 }
 
-#ifndef BLS_LINES_INL
-#define BLS_LINES_INL 2
-#endif
 
-// Call-free Miller steps (k_miller_lines at 2 waves/SIMD, BLS_LINES_INL == 2): every product expanded
+// Call-free Miller steps (k_miller_lines at 2 waves/SIMD): every product expanded
 // in place, one after the other (fenced), ordered so that few values are live at once, and each
 // line coefficient handed to put(c, v) (c = 0: l00, 1: l01, 2: l11) as soon as it is known; xp()/yp()
 // and the addition's q() re-read their operands at the use. Same operations on the same values as
-// miller_dbl_step / miller_add_step (BLS_LINES_FOLD: 3 xP, -yP and -xP folded into the radix-2^28
-// operand, the same residues in possibly another representative below 2p).
-#ifndef BLS_LINES_FOLD
-#define BLS_LINES_FOLD 0  // A/B profiles/r03s_lines_fold_sqrt_inl_ab.json: ~1 ms slower (scratch 504 -> 516 B)
-#endif
-// a * b for b handed over as radix-2^28 limbs that the caller has scaled by 3 or negated limb-wise
-// (fp_neg28: 16p - b): the line coefficients 3 X^2 xP, -H yP and -theta xP then cost no Fp2 mul3 or
-// negation. Limbs < 3 * 2^28 keep every column sum of fp_mont_dot below 2^63, and a product of
-// values < 2p and < 16p is < 2p after the reduction (R = 2^392), as fp2_mul's negated operand is.
-DI fp2 fp2_mul_fp28_inl(const fp2& a, const uint32_t (&y)[14]) {
-  BLS_COUNT_MUL();
-  BLS_COUNT_MUL();
-  uint32_t x[14];
-  fp_split28(fp_to_u12(a.c0), x);
-  const fp c0 = fp_from_u12(fp_mont_dot<false>(x, y, x, y));
-  BLS_SCHED_FENCE();
-  fp_split28(fp_to_u12(a.c1), x);
-  return {c0, fp_from_u12(fp_mont_dot<false>(x, y, x, y))};
-}
-DI void fp_split28_x3(const fp& a, uint32_t (&y)[14]) {
-  fp_split28(fp_to_u12(a), y);
-#pragma unroll
-  for (int k = 0; k < 14; k++) y[k] *= 3u;
-}
-DI void fp_split28_neg(const fp& a, uint32_t (&y)[14]) {
-  uint32_t v[14];
-  fp_split28(fp_to_u12(a), v);
-  fp_neg28(v, y);
-}
+// miller_dbl_step / miller_add_step.
 
 // The running point T of the call-free steps is reached through an accessor: TS::get(c) / set(c, v)
 // for c = 0, 1, 2 (X, Y, Z). TReg keeps T in registers; k_miller_lines parks it in LDS (its
@@ -109,15 +78,7 @@ DI void miller_dbl_step_ts(const TS& t, Put put, XP xp, YP yp) {
   BLS_SCHED_FENCE();
   const fp2 H = fp2_sub(fp2_sqr_inl(fp2_add_lazy(t.get(1), t.get(2))), fp2_add(B, C));
   BLS_SCHED_FENCE();
-#if BLS_LINES_FOLD
-  {
-    uint32_t y[14];
-    fp_split28_neg(yp(), y);
-    put(2, fp2_mul_fp28_inl(H, y));
-  }
-#else
   put(2, fp2_neg(fp2_mul_fp_inl(H, yp())));
-#endif
   BLS_SCHED_FENCE();
   t.set(2, fp2_mul_inl(B, H));  // Z3 (Z has had its last use)
   BLS_SCHED_FENCE();
@@ -128,16 +89,7 @@ DI void miller_dbl_step_ts(const TS& t, Put put, XP xp, YP yp) {
   const fp2 BF = fp2_sub(B, F);
   const fp2 A = fp2_half(fp2_mul_inl(t.get(0), t.get(1)));
   BLS_SCHED_FENCE();
-#if BLS_LINES_FOLD
-  {
-    const fp2 X2 = fp2_sqr_inl(t.get(0));
-    uint32_t y[14];
-    fp_split28_x3(xp(), y);
-    put(1, fp2_mul_fp28_inl(X2, y));
-  }
-#else
   put(1, fp2_mul_fp_inl(fp2_mul3(fp2_sqr_inl(t.get(0))), xp()));
-#endif
   BLS_SCHED_FENCE();
   t.set(0, fp2_mul_inl(A, BF));  // X3
   BLS_SCHED_FENCE();
@@ -160,20 +112,9 @@ DI void miller_add_step_ts(const TS& t, Q qload, Put put, XP xp, YP yp) {
     put(0, fp2_sub(u, fp2_mul_inl(delta, q.y)));
     BLS_SCHED_FENCE();
   }
-#if BLS_LINES_FOLD
-  {
-    uint32_t y[14];
-    fp_split28_neg(xp(), y);
-    put(1, fp2_mul_fp28_inl(theta, y));
-    BLS_SCHED_FENCE();
-    fp_split28(fp_to_u12(yp()), y);
-    put(2, fp2_mul_fp28_inl(delta, y));
-  }
-#else
   put(1, fp2_neg(fp2_mul_fp_inl(theta, xp())));
   BLS_SCHED_FENCE();
   put(2, fp2_mul_fp_inl(delta, yp()));
-#endif
   BLS_SCHED_FENCE();
   const fp2 C = fp2_sqr_inl(theta);
   BLS_SCHED_FENCE();
@@ -302,7 +243,7 @@ DI void miller_lines(const g1a& P, LoadQ load_q, Emit emit) {
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
     line l;
-    miller_dbl_step<BLS_LINES_INL == 1>(T, l.a0, l.a1, l.a4, P.x, P.y);
+    miller_dbl_step<false>(T, l.a0, l.a1, l.a4, P.x, P.y);
     emit(step++, l);
     if ((BLS_X_ABS >> i) & 1ull) {
       miller_add_step(T, load_q(), l.a0, l.a1, l.a4, P.x, P.y);
@@ -412,132 +353,6 @@ DI fp12 final_exponentiation(const fp12& f) {
   const fp12 c = fexp_step<2>([&]() { return b; }, none, none);
   const fp12 t = fexp_step<3>([&]() { return c; }, none, none);
   return fexp_step<4>([&]() { return t; }, [&]() { return c; }, [&]() { return g; });
-}
-
-// ---------------------------------------------------------------- compressed cyclotomic squaring
-// Karabina (eprint 2010/542) for X in the cyclotomic subgroup, in the w-power basis f = sum c_k w^k:
-// the squaring of (c1, c2, c4, c5) never needs c0 or c3. With A1 = c1 + c4 s, A2 = c2 + c5 s
-// (Fp4 = Fp2[s], s = w^3, s^2 = xi) and Y_j = A_j^2:
-//   c1' = 2 c1 + 3 xi Y2.b   c4' = 3 Y2.a - 2 c4   c2' = 3 Y1.a - 2 c2   c5' = 2 c5 + 3 Y1.b
-// i.e. the Granger-Scott square restricted to the thirds A1, A2 (tri.h roles 1 and 2): 6 Fp2 squares
-// instead of 9. Decompression recovers the dropped coefficients (identities checked against the
-// oracle's Fp12 arithmetic on random cyclotomic elements, tests/test_abi.py):
-//   c3 = (xi c5^2 + 3 c2^2 - 2 c4) / (4 c1)       (c1 != 0)
-//   c3 = 2 c2 c5 / c4                            (c1 == 0: c3 c4 - 2 c2 c5 = c1 (1 - i)(1 - c0) / 2)
-//   c0 = xi (2 c3^2 + c1 c5 - 3 c4 c2) + 1
-// and c1 = c4 = 0 only for X = 1 (numerator 0 over denominator 1 then gives c3 = 0, c0 = 1).
-// X^|x| = prod_b X^(2^b) over the set bits b = 16, 48, 57, 60, 62, 63 of |x|: 63 compressed squares,
-// six decompressions sharing one Fp2 inversion (Montgomery's trick), 5 multiplications.
-struct fp12c {
-  fp2 c1, c4, c2, c5;  // A1 = (c1, c4), A2 = (c2, c5)
-};
-
-DI fp12c fp12_compress(const fp12& x) { return {x.c1.c0, x.c0.c2, x.c0.c1, x.c1.c2}; }
-
-// (a + b s)^2 = (a^2 + xi b^2) + 2ab s as (square part, cross part): 3 Fp2 squares. INL: the squares
-// expanded in place, one after the other (call-free squaring kernels, k_fexp.hip)
-template <bool INL = false>
-DI void fp4_sqr_parts(const fp2& a, const fp2& b, fp2& sq, fp2& cross) {
-  auto sqr = [](const fp2& v) { return INL ? fp2_sqr_inl(v) : fp2_sqr(v); };
-  const fp2 t0 = sqr(a);
-  BLS_SCHED_FENCE();
-  const fp2 t1 = sqr(b);
-  BLS_SCHED_FENCE();
-  const fp2 t2 = sqr(fp2_add_lazy(a, b));
-  BLS_SCHED_FENCE();
-  sq = fp2_add(t0, fp2_mul_xi(t1));
-  cross = fp2_sub(t2, fp2_add(t0, t1));
-}
-
-template <bool INL = false>
-DI fp12c karabina_sqr(const fp12c& x) {
-  fp2 y1a, y1b, y2a, y2b;
-  fp4_sqr_parts<INL>(x.c1, x.c4, y1a, y1b);
-  fp4_sqr_parts<INL>(x.c2, x.c5, y2a, y2b);
-  return {fp2_add(fp2_dbl(x.c1), fp2_mul3(fp2_mul_xi(y2b))), fp2_sub(fp2_mul3(y2a), fp2_dbl(x.c4)),
-          fp2_sub(fp2_mul3(y1a), fp2_dbl(x.c2)), fp2_add(fp2_dbl(x.c5), fp2_mul3(y1b))};
-}
-
-// The third A0 = c0 + c3 s evolves on its own under the cyclotomic square (tower.h
-// fp12_cyclotomic_sqr: z0, z1 depend only on A0^2): (c0, c3) <- (3 Y.a - 2 c0, 3 Y.b + 2 c3), Y = A0^2.
-// With karabina_sqr this is the whole Granger-Scott square, split into two independent chains.
-template <bool INL = false>
-DI void cyclotomic_sqr_a0(fp2& c0, fp2& c3) {
-  fp2 ya, yb;
-  fp4_sqr_parts<INL>(c0, c3, ya, yb);
-  c0 = fp2_sub(fp2_mul3(ya), fp2_dbl(c0));
-  c3 = fp2_add(fp2_mul3(yb), fp2_dbl(c3));
-}
-
-// numerator / denominator of c3 (branch-free selection of the three cases above)
-DI void karabina_num_den(const fp12c& x, fp2& num, fp2& den) {
-  const bool z1 = fp2_is_zero(x.c1), z4 = fp2_is_zero(x.c4);
-  const fp2 n_main = fp2_sub(fp2_add(fp2_mul_xi(fp2_sqr(x.c5)), fp2_mul3(fp2_sqr(x.c2))), fp2_dbl(x.c4));
-  const fp2 n_alt = fp2_dbl(fp2_mul(x.c2, x.c5));
-  num = fp2_select(z1, fp2_select(z4, fp2_zero(), n_alt), n_main);
-  den = fp2_select(z1, fp2_select(z4, fp2_one(), x.c4), fp2_dbl(fp2_dbl(x.c1)));
-}
-
-// c0 from the other five coefficients
-DI fp2 karabina_c0(const fp12c& x, const fp2& c3) {
-  const fp2 t = fp2_sub(fp2_add(fp2_dbl(fp2_sqr(c3)), fp2_mul(x.c1, x.c5)), fp2_mul3(fp2_mul(x.c4, x.c2)));
-  return fp2_add(fp2_mul_xi(t), fp2_one());
-}
-
-DI fp12 fp12_from_compressed(const fp12c& x, const fp2& c0, const fp2& c3) { return {{c0, x.c2, x.c4}, {x.c1, c3, x.c5}}; }
-
-constexpr int KARABINA_N = 6;  // set bits of |x|
-// squaring count after which X^(2^b) is kept, b = 16, 48, 57, 60, 62, 63 (one bit each of KARABINA_KEEP)
-constexpr uint64_t KARABINA_KEEP = BLS_X_ABS;
-
-// X^|x| in registers (host op counter, test hook): the device runs the same three phases as kernels
-// (k_fexp.hip: duo squaring chain, one-lane batch decompression, 3-lane products)
-DI fp12 fp12_pow_x_abs_karabina(const fp12& X) {
-  fp12c c = fp12_compress(X);
-  fp12c S[KARABINA_N];
-  int e = 0;
-  for (int k = 1; k <= 63; k++) {
-    c = karabina_sqr(c);
-    if ((KARABINA_KEEP >> k) & 1ull) S[e++] = c;
-  }
-  fp2 num[KARABINA_N], den[KARABINA_N], pre[KARABINA_N];
-  for (int j = 0; j < KARABINA_N; j++) {
-    karabina_num_den(S[j], num[j], den[j]);
-    pre[j] = j ? fp2_mul(pre[j - 1], den[j]) : den[j];
-  }
-  fp2 inv = fp2_inv(pre[KARABINA_N - 1]);
-  fp12 r = fp12_one();
-  for (int j = KARABINA_N - 1; j >= 0; j--) {
-    const fp2 dinv = j ? fp2_mul(inv, pre[j - 1]) : inv;
-    if (j) inv = fp2_mul(inv, den[j]);
-    const fp2 c3 = fp2_mul(num[j], dinv);
-    const fp12 D = fp12_from_compressed(S[j], karabina_c0(S[j], c3), c3);
-    r = j == KARABINA_N - 1 ? D : fp12_mul(r, D);
-  }
-  return r;
-}
-
-// fexp_step<MODE> with X^|x| from the compressed chain
-template <int MODE, typename LX, typename LC, typename LG>
-DI fp12 fexp_step_karabina(LX lx, LC lc, LG lg) {
-  fp12 r = fp12_conj(fp12_pow_x_abs_karabina(lx()));
-  if (MODE == 0 || MODE == 1) return fp12_mul(r, fp12_conj(lx()));
-  if (MODE == 2) return fp12_mul(r, fp12_frob(lx()));
-  if (MODE == 3) return r;
-  r = fp12_mul(r, fp12_frob2(lc()));
-  r = fp12_mul(r, fp12_conj(lc()));
-  r = fp12_mul(r, fp12_cyclotomic_sqr(lg()));
-  return fp12_mul(r, lg());
-}
-
-DI fp12 final_exponentiation_karabina(const fp12& f) {
-  const fp12 g = fexp_easy(f);
-  auto none = [&]() { return g; };
-  const fp12 a = fexp_step_karabina<0>([&]() { return g; }, none, none);
-  const fp12 b = fexp_step_karabina<1>([&]() { return a; }, none, none);
-  const fp12 c = fexp_step_karabina<2>([&]() { return b; }, none, none);
-  const fp12 t = fexp_step_karabina<3>([&]() { return c; }, none, none);
-  return fexp_step_karabina<4>([&]() { return t; }, [&]() { return c; }, [&]() { return g; });
 }
 
 }  // namespace bls

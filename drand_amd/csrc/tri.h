@@ -24,9 +24,6 @@ namespace bls {
 constexpr int TRI_GROUPS = 21;  // beacons per 64-lane wave
 
 // role-dependent additions as one fp_addsub (direction as data) instead of both results + a select
-#ifndef BLS_TRI_ADDSUB
-#define BLS_TRI_ADDSUB 1
-#endif
 
 struct fp4 {
   fp2 a, b;  // a + b s
@@ -158,29 +155,16 @@ DI fp4 tri_conj(const tri_lane& t, const fp4& x) {
 // each lane squares its Fp4 (X = A_j^2); roles 1 and 2 swap their squares; then
 //   role 0, 2: (a, b) <- (3 Y.a - 2 a, 3 Y.b + 2 b)     (role 0: Y = own square, role 2: role 1's)
 //   role 1:    (a, b) <- (3 xi Y.b + 2 a, 3 Y.a - 2 b)  (Y = role 2's square)
-#ifndef BLS_FP4_SQR_DOT
-#define BLS_FP4_SQR_DOT 1
-#endif
 DI fp4 tri_cyclotomic_sqr(const tri_lane& t, const fp4& x) {
-#if BLS_FP4_SQR_DOT
   const fp4 sq = fp4_sqr_dot(x);
-#else
-  const fp4 sq = fp4_sqr_inl(x);
-#endif
   const int src = t.role == 1 ? t.next_b : (t.role == 2 ? t.prev_b : (int)(4u * t.lane));
   const fp4 y = xchg_fp4(sq, src);
   const bool r1 = t.role == 1;
   const fp2 u = fp2_select(r1, fp2_mul_xi(y.b), y.a);
   const fp2 v = fp2_select(r1, y.a, y.b);
-#if BLS_TRI_ADDSUB
   // 3u +- 2a = 2(u +- a) + u: one direction-by-role addition instead of both and a select
   const fp2 ta = fp2_addsub(u, x.a, !r1), tb = fp2_addsub(v, x.b, r1);
   return {fp2_add(fp2_dbl(ta), u), fp2_add(fp2_dbl(tb), v)};
-#else
-  const fp2 u3 = fp2_add(fp2_dbl(u), u), v3 = fp2_add(fp2_dbl(v), v);
-  const fp2 a2 = fp2_dbl(x.a), b2 = fp2_dbl(x.b);
-  return {fp2_select(r1, fp2_add(u3, a2), fp2_sub(u3, a2)), fp2_select(r1, fp2_sub(v3, b2), fp2_add(v3, b2))};
-#endif
 }
 
 // general product (Karatsuba over the cubic): lane j forms P_j = A_j B_j and
@@ -386,20 +370,12 @@ DI fp4 tri_mul_lp(const tri_lane& t, const fp4& a, const fp4& b, uint32_t* park,
   {
     const fp4 Pn = xchg_fp4(P, t.next_b);
     const fp4 u = fp4_select(t.role == 2, Pn, fp4_mul_s(Pn));
-#if BLS_TRI_ADDSUB
     R = fp4_addsub(R, u, t.role != 1);
-#else
-    R = fp4_add(R, fp4_select(t.role == 1, u, fp4_neg(u)));
-#endif
   }
   {
     const fp4 Pp = xchg_fp4(P, t.prev_b);
     const fp4 u = fp4_select(t.role == 0, fp4_mul_s(Pp), Pp);
-#if BLS_TRI_ADDSUB
     R = fp4_addsub(R, u, t.role != 2);
-#else
-    R = fp4_add(R, fp4_select(t.role == 2, u, fp4_neg(u)));
-#endif
   }
   {
     size_t j = park_i;
@@ -432,37 +408,6 @@ DI fp4 tri_frob2(const tri_lane& t, const fp4& x) {
   ga = fp_select(j == 1, fp_load_const(FROB2_GAMMA[1][0]), fp_select(j == 2, fp_load_const(FROB2_GAMMA[2][0]), ga));
   gb = fp_select(j == 1, fp_load_const(FROB2_GAMMA[4][0]), fp_select(j == 2, fp_load_const(FROB2_GAMMA[5][0]), gb));
   return {fp2_mul_fp(x.a, ga), fp2_mul_fp(x.b, gb)};
-}
-
-// ------------------------------------------------------------------ two lanes per Fp12 ("duo")
-// The compressed cyclotomic square (pairing.h karabina_sqr) touches only the thirds A1 = (c1, c4) and
-// A2 = (c2, c5): lane pair (2j, 2j + 1) holds A1 (role 1, even lane) and A2 (role 2) of beacon j, 32
-// beacons per wave and no idle lane. The partner's square crosses over DPP quad_perm [1, 0, 3, 2]
-// (one VALU move per word, no LDS round trip).
-constexpr int DUO_GROUPS = 32;
-DI fp duo_swap(const fp& v) {
-  fp r;
-#pragma unroll
-  for (int i = 0; i < 12; i++) r.l[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.l[i], 0xB1, 0xf, 0xf, false);
-  return r;
-}
-DI fp2 duo_swap2(const fp2& v) { return {duo_swap(v.c0), duo_swap(v.c1)}; }
-
-// tri_cyclotomic_sqr for roles 1 and 2 only (role 1: r1 = true), call-free:
-//   role 1: (c1, c4) <- (2 c1 + 3 xi Y2.b, 3 Y2.a - 2 c4)   role 2: (c2, c5) <- (3 Y1.a - 2 c2, 2 c5 + 3 Y1.b)
-DI fp4 duo_karabina_sqr(bool r1, const fp4& x) {
-  // the three squares one after the other (fenced): interleaved, they would double the live set
-  const fp2 t0 = fp2_sqr_inl(x.a);
-  BLS_SCHED_FENCE();
-  const fp2 t1 = fp2_sqr_inl(x.b);
-  BLS_SCHED_FENCE();
-  const fp2 t2 = fp2_sqr_inl(fp2_add_lazy(x.a, x.b));
-  BLS_SCHED_FENCE();
-  const fp4 sq = {fp2_add(t0, fp2_mul_xi(t1)), fp2_sub(fp2_sub(t2, t0), t1)};
-  const fp2 ya = duo_swap2(sq.a), yb = duo_swap2(sq.b);
-  const fp2 u3 = fp2_mul3(fp2_select(r1, fp2_mul_xi(yb), ya)), v3 = fp2_mul3(fp2_select(r1, ya, yb));
-  const fp2 a2 = fp2_dbl(x.a), b2 = fp2_dbl(x.b);
-  return {fp2_select(r1, fp2_add(u3, a2), fp2_sub(u3, a2)), fp2_select(r1, fp2_sub(v3, b2), fp2_add(v3, b2))};
 }
 
 // this lane's part of "f == 1": role 0 must hold (1, 0), roles 1, 2 zero; combined over the group

@@ -154,11 +154,11 @@ def test_threshold_partials_and_recover(engine, golden):
 
 
 def test_final_exp_tri_matches_one_lane(engine):
-    """The production final exponentiation (compressed squaring chain on 2 lanes per Fp12,
-    k_fexp_ksq; batch decompression, k_fexp_kdec; products on 3 lanes, k_fexp_tri) equals the
-    one-lane Granger-Scott register form (pairing.h final_exponentiation, itself pinned by the pairing
-    goldens) on random Fp12 values, including batches that are not a multiple of the 21 (3-lane) or
-    32 (2-lane) beacons per wave. The identity exercises the c1 = c4 = 0 decompression case."""
+    """The production final exponentiation (k_fexp_easy on one lane per Fp12, then the hard part's
+    five steps k_fexp_tri<0..4>: Granger-Scott cyclotomic squares and products with each Fp12 spread
+    over 3 lanes, 21 beacons per wave) equals the one-lane register form (pairing.h
+    final_exponentiation, itself pinned by the pairing goldens) on random Fp12 values, including
+    batches that are not a multiple of 21 and the identity."""
     import random
     from oracle import bls12381 as O
     rng = random.Random(5)
