@@ -215,6 +215,13 @@ def main():
     else:
         torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
+    # One explicit stream for the engine AND the torch ops around it (the exchange's placement and
+    # all-reduce): the C ABI's NULL stream means the context's own non-blocking stream, which torch's
+    # default stream does not wait for.
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    assert sp, "the engine stream must be an explicit stream"
 
     from drand_amd import shard
     from drand_amd.engine import Engine
@@ -265,8 +272,6 @@ def main():
 
     eng = Engine(dev_idx)
     eng.set_public_key(pk48)
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
     t_gen = time.perf_counter()
     eng.generate_chained_dev(sk32, gen_first_round, seg, gen_seeds.data_ptr(), gen_seed0_len, gen_sigs.data_ptr(),
                              gen_n, sp)
