@@ -23,7 +23,6 @@ import os
 
 import pytest
 
-from drand_amd import _lib
 
 pytestmark = pytest.mark.gpu
 
@@ -214,8 +213,8 @@ def test_chained_dev_latency_branch(engine, golden, C, n, seg, phase, first_roun
 def test_verify_partials_256_mixed(engine, golden, C):
     """k = 256 partials of one round: the 64 golden shares four times in shuffled orders, with
     corruptions (bit flip, a decode class, a share presented under another index, an index >= n,
-    a wrong-length-free V2 share of the wrong message) -- every class equal on both paths and to
-    the C oracle's tbls VerifyPartial."""
+    the V2 share of the same signer, which signs MessageV2) -- every class equal on all three
+    routes and to the C oracle's tbls VerifyPartial."""
     import random
 
     th = golden["threshold"]
@@ -241,10 +240,9 @@ def test_verify_partials_256_mixed(engine, golden, C):
     d, b, l = _routes(engine, lambda: engine.verify_partials(msg, batch), len(batch))
     assert d == b == l
     ok, cls = d
-    idx_bad = [i for i, p in enumerate(batch) if int.from_bytes(p[:2], "big") >= th["n"]]
-    assert [cls[i] for i in idx_bad] == [_lib.REJ_SHARE_INDEX] * len(idx_bad)
-    assert [c != 0 for c in cls] == [c != 0 for c in want]
-    assert [c for i, c in enumerate(cls) if i not in idx_bad] == [c for i, c in enumerate(want) if i not in idx_bad]
+    # an index >= n is no error of its own in tbls VerifyPartial (PubPoly.Eval(i) at any i): the
+    # share simply fails the pairing check under that index's public share, as in the C oracle
+    assert cls == want
     assert ok == [c == 0 for c in cls]
 
 
