@@ -75,6 +75,7 @@ SIGNATURES = {
     "blsv_generate_chained_dev": (ctypes.c_int, [vp, u8p, ctypes.c_uint64, ctypes.c_uint64, vp, sz, vp, sz, vp]),
     "blsv_profile_enable": (ctypes.c_int, [vp, ctypes.c_int]),
     "blsv_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), u64p, u64p, ctypes.c_int]),
+    "blsv_lat_trace": (ctypes.c_int, [vp, u64p, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "blsv_test_fp_mul": (ctypes.c_int, [vp, u32p, u32p, sz, u32p]),
     "blsv_test_pairing": (ctypes.c_int, [vp, u32p, u32p, sz, u32p]),
     "blsv_test_hash_to_g2": (ctypes.c_int, [vp, u8p, u32p, sz, u32p, u8p]),

@@ -992,6 +992,25 @@ int blsv_profile_read(blsv_ctx* c, double* ms, uint64_t* launches, uint64_t* ite
   return ST_N;
 }
 
+int blsv_lat_trace(blsv_ctx* c, uint64_t* ticks, int n, double* ticks_per_us, int clear) {
+  if (!c || n < 0 || (n && !ticks)) return BLSV_EINVAL;
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int got = 0;
+  if (n) {
+    got = blsk::lat_trace_read(ticks, n, c->stream);
+    if (got < 0) return fail(c, BLSV_EHIP, "lat_trace: symbol copy failed");
+  }
+  if (ticks_per_us) {
+    int khz = 0;
+    HIPCHK(c, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    *ticks_per_us = khz / 1000.0;
+  }
+  if (clear && blsk::lat_trace_clear(c->stream) != 0) return fail(c, BLSV_EHIP, "lat_trace: clear failed");
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return got;
+}
+
 // latency-path cutover (include/blsverify.h latency contract)
 size_t blsv_set_lat_max(blsv_ctx* c, size_t lat_max) {
   if (!c) return 0;

@@ -7,6 +7,10 @@
 #include "kcommon.h"
 #include "wvteam.h"
 
+namespace wv {
+__device__ uint64_t g_lat_trace[LAT_TRACE_N];
+}
+
 namespace blsk {
 
 __constant__ uint8_t c_lat_dst[DST_LEN] = {66, 76, 83, 95, 83, 73, 71, 95, 66, 76, 83, 49, 50, 51, 56, 49, 71, 50, 95, 88,
@@ -90,6 +94,22 @@ __global__ void __launch_bounds__(256) k_lat_messages(const uint8_t* msgs, const
   if (i >= cnt) return;
   lat_verify([&](uint32_t(&b0)[8]) { xmd_b0_bytes(b0, msgs + off[i], len[i], c_lat_dst); }, i,
              sigs + i * stride + offset, pk_tab, pk_inf, pk_idx, cls, S, s_inf, cnt);
+}
+
+// the phase marks of the last latency launch's item 0 (wteam.h WV_MARK), device wall-clock ticks
+int lat_trace_read(uint64_t* out, int n, hipStream_t st) {
+  if (n > wv::LAT_TRACE_N) n = wv::LAT_TRACE_N;
+  if (hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(wv::g_lat_trace), n * sizeof(uint64_t), 0, hipMemcpyDeviceToHost, st) !=
+      hipSuccess)
+    return -1;
+  if (hipStreamSynchronize(st) != hipSuccess) return -1;
+  return n;
+}
+int lat_trace_clear(hipStream_t st) {
+  static const uint64_t z[wv::LAT_TRACE_N] = {};
+  return hipMemcpyToSymbolAsync(HIP_SYMBOL(wv::g_lat_trace), z, sizeof z, 0, hipMemcpyHostToDevice, st) == hipSuccess
+             ? 0
+             : -1;
 }
 
 void launch_lat_chained(const ChainedSrc& src, size_t base, size_t cnt, const uint32_t* pk_tab, const uint8_t* pk_inf,

@@ -170,7 +170,9 @@ WVI bool team_final_exp_is_one(Team& t, int f0) {
   team_op(t, W_U, [&](int k) { return w12_frob2_c(xld_w12(W_T), k); });
   team_op(t, W_G, [&](int k) { return w12_mul_c(xld_w12(W_U), xld_w12(W_T), k); });
   // a = g^(x-1), b = a^(x-1), c = b^(x+p); X^x = conj(X^|x|)
+  if (t.id == 0) WV_MARK(8);
   team_pow_x_abs(t, W_P, W_G, W_S);
+  if (t.id == 0) WV_MARK(9);
   team_op(t, W_A, [&](int k) { return w12_mul_c(xld_w12(W_P, true), xld_w12(W_G, true), k); });
   team_pow_x_abs(t, W_P, W_A, W_S);
   team_op(t, W_B, [&](int k) { return w12_mul_c(xld_w12(W_P, true), xld_w12(W_A, true), k); });
@@ -196,9 +198,11 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
                         bool pk_inf, F& sx, F& sy, bool& s_inf) {
   const int w = wave_id();
   Team all = make_team(0, 4, 0);
+  if (w == 0) WV_MARK(0);
   if (w == 0) {
     F hx, hy;
     const bool fin = hash_to_g2(b0, hx, hy);
+    WV_MARK(1);
     if (fin) {
       xst(S_HX, hx);
       xst(S_HY, hy);
@@ -210,6 +214,7 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
       F x, y;
       bool inf;
       const uint8_t c = g2_decompress(sig, x, y, inf);
+      WV_MARK(2);
       if (c == bls::REJ_OK && !inf) {
         xst(S_SX, x);
         xst(S_SY, y);
@@ -222,9 +227,11 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
       const MPair m1 = mpair(cst(WC_NEG_G1_X), cst(WC_NEG_G1_Y), xld(S_SX), xld(S_SY));
       const int f1 = team_miller(t1, m1, TB1);
       if (t1.id == 0) xst_word(XW_F1, (uint32_t)f1);
+      if (t1.id == 0) WV_MARK(3);
     }
   }
   team_sync(all);
+  if (w == 0) WV_MARK(4);
   const uint8_t cls = (uint8_t)xld_word(XW_CLS);
   if (cls != bls::REJ_OK) return cls;
   s_inf = xld_word(XW_SINF) != 0;
@@ -238,6 +245,7 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
   if (a0) {
     const MPair m0 = mpair(g1_coord(pkx), g1_coord(pky), xld(S_HX), xld(S_HY));
     f = team_miller(all, m0, TB0);
+    if (w == 0) WV_MARK(5);
     if (a1) {
       const int f1 = (int)xld_word(XW_F1);
       team_op(all, W_R, [&](int k) { return w12_mul_c(xld_w12(f), xld_w12(f1), k); });
@@ -246,7 +254,10 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
   } else {
     f = (int)xld_word(XW_F1);
   }
-  return team_final_exp_is_one(all, f) ? bls::REJ_OK : bls::REJ_PAIRING;
+  if (w == 0) WV_MARK(6);
+  const bool one = team_final_exp_is_one(all, f);
+  if (w == 0) WV_MARK(7);
+  return one ? bls::REJ_OK : bls::REJ_PAIRING;
 }
 
 }  // namespace wv

@@ -303,6 +303,21 @@ class Engine:
             raise EngineError(rc, self.lib.blsv_last_error(self._h).decode())
         return {s: (ms[k], la[k], it[k]) for k, s in enumerate(self.STAGES)}
 
+    LAT_MARKS = ("start", "hash", "sig_decoded", "sig_miller", "phase_a", "key_miller", "miller_product",
+                 "final_exp", "pow1_start", "pow1_end")
+
+    def lat_trace(self, clear=True):
+        """Phase marks (microseconds from the first mark) of item 0 of the last latency-path launch
+        (blsv_lat_trace); marks never stamped are left out."""
+        n = len(self.LAT_MARKS)
+        t = (ctypes.c_uint64 * n)()
+        rate = ctypes.c_double()
+        got = self.lib.blsv_lat_trace(self._h, t, n, ctypes.byref(rate), 1 if clear else 0)
+        if got < 0:
+            raise EngineError(got, self.lib.blsv_last_error(self._h).decode())
+        t0 = t[0]
+        return {k: (t[i] - t0) / rate.value for i, k in enumerate(self.LAT_MARKS[:got]) if t[i] and t0}
+
     # ------------------------------------------------------------------ testing hooks
     def set_lat_max(self, n):
         """Batches of at most n items take the latency path (one wave per item); returns the old cutover."""

@@ -6,8 +6,10 @@
   aggregator round      (blsv_aggregate: 64 partials, Recover from 33, VerifyRecovered)
 
 Each is the median wall clock over `reps` calls from the host API, plus the per-stage GPU time of
-one call (HIP events on the launch stream, blsv_profile_*). Inputs are the committed golden vectors
-(tests/golden/golden.json); every result is checked against them.
+one call (HIP events on the launch stream, blsv_profile_*) and, for the lone verify, the phase marks
+of the latency kernel (blsv_lat_trace). Inputs are the committed golden vectors
+(tests/golden/golden.json); every result is checked against them. The C oracle's single-thread lone
+verify of the same beacon is timed on the same host as the CPU baseline.
 
 --sweep N1,N2,..: also time blsv_verify_messages of N distinct device-signed messages through the
 latency path and through the batch pipeline (the BLSV_LAT_MAX cutover is where they cross).
@@ -79,6 +81,9 @@ def main():
 
         med, mn = timed(lone_beacon, a.reps)
         out["lone_verify_beacon"] = {"median_ms": med, "min_ms": mn, "stages_ms": stages(eng, lone_beacon)}
+        eng.lat_trace(clear=True)
+        lone_beacon()
+        out["lone_verify_beacon"]["phases_us"] = {k: round(v, 1) for k, v in eng.lat_trace().items()}
 
         eng.set_group(commits, th["n"])
 
@@ -125,6 +130,18 @@ def main():
                 print(json.dumps(row), flush=True)
             eng.set_lat_max(cur)
             out["cutover_sweep"] = sweep
+    # CPU baseline of the same lone call: the C oracle (oracle/c/bls_oracle.c, a plain-C port of the
+    # kilic algorithms without its assembly) on ONE host thread -- what one kyber verify per arrival
+    # costs a core, to set beside the GPU's per-arrival latency
+    from oracle import c_oracle  # checker / baseline only
+    c_oracle.load()
+    pk48 = bytes.fromhex(ch["pk"])
+
+    def cpu_lone():
+        assert c_oracle.verify_chained(pk48, 2, sigs[0], sigs[1]) == [0]
+
+    med, mn = timed(cpu_lone, max(3, a.reps // 2))
+    out["cpu_lone_verify_beacon"] = {"median_ms": med, "min_ms": mn, "threads": 1, "kind": "port (C oracle)"}
     line = json.dumps(out)
     print(line)
     if a.out:
