@@ -12,6 +12,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of bench.py with BLSV_SERIAL_STAGES=1
 #   pmc              PMC passes: FETCH_SIZE, WRITE_SIZE, two SQ/GRBM sets (tools/pmc_sq.py)
 #   cabi             tools/cabi_smoke (latency contract from plain C)
+#   intrate          tools/intrate (peak v_mad_u64_u32 rate) and its SQ/GRBM counters (clock of the peak)
 #   lat              tools/latency_bench.py (lone verify, fused round, crossover sweep)
 #   cfg              tools/config_bench.py (configs[2], configs[4], partials, drand.db)
 #   variant:NAME     GPU suite + bench on variants/libblsverify_NAME.so (scripts/build_variant.sh,
@@ -56,7 +57,13 @@ for step in "$@"; do
       python3 tools/pmc_sq.py "$O/pmc_sq.json" "$O/pmc_a/run_counter_collection.csv" \
         "$O/pmc_b/run_counter_collection.csv" > /dev/null &&
       python3 tools/pmc_traffic.py "$O/pmc_fetch/run_counter_collection.csv" \
-        "$O/pmc_write/run_counter_collection.csv" 262144 "$O/pmc_traffic.json" > /dev/null || rc=16 ;;
+        "$O/pmc_write/run_counter_collection.csv" 786432 "$O/pmc_traffic.json" > /dev/null || rc=16 ;;
+    intrate)
+      make -s -C tools intrate > /dev/null &&
+      timeout -k 10 120 tools/intrate > "$O/intrate.txt" 2>&1 &&
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE \
+        --output-format csv -d "$O/pmc_intrate" -o run -- tools/intrate > "$O/pmc_intrate.log" 2>&1 &&
+      python3 tools/pmc_sq.py "$O/pmc_intrate.json" "$O/pmc_intrate/run_counter_collection.csv" > /dev/null || rc=23 ;;
     cabi) timeout -k 10 120 tools/cabi_smoke > "$O/cabi_smoke.txt" 2>&1 || rc=20 ;;
     lat) timeout -k 10 300 python -u tools/latency_bench.py --reps 10 --out "$O/latency.json" > "$O/latency.log" 2>&1 || rc=21 ;;
     cfg) timeout -k 10 600 python -u tools/config_bench.py > "$O/config_bench.json" 2> "$O/config_bench.log" || rc=22 ;;
