@@ -19,7 +19,10 @@
 namespace {
 
 constexpr size_t kMaxChunk = size_t(1) << 20;  // beacons per pipeline pass (~1 GB of staging)
-constexpr size_t kLineSub = size_t(1) << 17;   // Miller line staging: 128 Ki beacons x 39 KB = 5.1 GB
+#ifndef BLS_LINE_SUB_LOG2
+#define BLS_LINE_SUB_LOG2 17
+#endif
+constexpr size_t kLineSub = size_t(1) << BLS_LINE_SUB_LOG2;  // Miller line staging: 128 Ki beacons x 39 KB = 5.1 GB
 
 struct DBuf {
   void* p = nullptr;

@@ -6,6 +6,11 @@
 
 namespace bls {
 
+#ifndef BLS_SOA_BUF
+#define BLS_SOA_BUF 0
+#endif
+
+#if defined(BLS_HOST) || !BLS_SOA_BUF
 DI void st_fp(uint32_t* buf, size_t n, size_t i, int slot, const fp& a) {
 #pragma unroll
   for (int k = 0; k < 12; k++) buf[(size_t)(slot * 12 + k) * n + i] = a.l[k];
@@ -16,6 +21,71 @@ DI fp ld_fp(const uint32_t* buf, size_t n, size_t i, int slot) {
 #pragma unroll
   for (int k = 0; k < 12; k++) a.l[k] = buf[(size_t)(slot * 12 + k) * n + i];
   return a;
+}
+#else
+// Buffer-resource form: the slot's 12 words are one resource (base = the slot's first column, at
+// most 12 n words), the item's byte offset i * 4 is the one VGPR offset and each word's k * n * 4 an
+// SGPR offset recomputed at its use (an opaque stride keeps LLVM from hoisting a kernel's hundreds
+// of distinct offsets into SGPRs it then spills) -- no 64-bit VGPR address per word.
+DI __amdgpu_buffer_rsrc_t soa_slot_rsrc(const uint32_t* buf, size_t n, int slot) {
+  const size_t bytes = (size_t)12 * n * 4;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(buf) + (size_t)slot * 12 * n, 0,
+                                           (int)(bytes < 0x7fffffffu ? bytes : 0x7fffffffu), 0x00020000);
+}
+DI uint32_t soa_word_off(size_t n, int k) {
+  uint32_t n4 = (uint32_t)(n * 4);
+  asm volatile("" : "+s"(n4));
+  return (uint32_t)k * n4;
+}
+DI void st_fp(uint32_t* buf, size_t n, size_t i, int slot, const fp& a) {
+  const __amdgpu_buffer_rsrc_t r = soa_slot_rsrc(buf, n, slot);
+#pragma unroll
+  for (int k = 0; k < 12; k++) __builtin_amdgcn_raw_buffer_store_b32(a.l[k], r, (uint32_t)(i * 4), soa_word_off(n, k), 0);
+}
+
+DI fp ld_fp(const uint32_t* buf, size_t n, size_t i, int slot) {
+  const __amdgpu_buffer_rsrc_t r = soa_slot_rsrc(buf, n, slot);
+  fp a;
+#pragma unroll
+  for (int k = 0; k < 12; k++) a.l[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(i * 4), soa_word_off(n, k), 0);
+  return a;
+}
+#endif
+
+// A lane-varying slot (the 3-lane layouts pick slots by lane role): the buffer form keeps ONE
+// resource over the whole object -- at most 12 Fp slots from `buf` (an Fp12, a line pair's six
+// slots) -- since a resource must be wave-uniform, and moves the slot into the VGPR offset; the
+// plain form is the same as st_fp / ld_fp.
+#if defined(BLS_HOST) || !BLS_SOA_BUF
+DI void st_fp_v(uint32_t* buf, size_t n, size_t i, int slot, const fp& a) { st_fp(buf, n, i, slot, a); }
+DI fp ld_fp_v(const uint32_t* buf, size_t n, size_t i, int slot) { return ld_fp(buf, n, i, slot); }
+#else
+DI __amdgpu_buffer_rsrc_t soa_obj_rsrc(const uint32_t* buf, size_t n, int slots) {
+  const size_t bytes = (size_t)slots * 12 * n * 4;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(buf), 0,
+                                           (int)(bytes < 0x7fffffffu ? bytes : 0x7fffffffu), 0x00020000);
+}
+DI void st_fp_v(uint32_t* buf, size_t n, size_t i, int slot, const fp& a) {
+  const __amdgpu_buffer_rsrc_t r = soa_obj_rsrc(buf, n, 12);
+  const uint32_t vo = (uint32_t)(((size_t)slot * 12 * n + i) * 4);
+#pragma unroll
+  for (int k = 0; k < 12; k++) __builtin_amdgcn_raw_buffer_store_b32(a.l[k], r, vo, soa_word_off(n, k), 0);
+}
+DI fp ld_fp_v(const uint32_t* buf, size_t n, size_t i, int slot) {
+  const __amdgpu_buffer_rsrc_t r = soa_obj_rsrc(buf, n, 12);
+  const uint32_t vo = (uint32_t)(((size_t)slot * 12 * n + i) * 4);
+  fp a;
+#pragma unroll
+  for (int k = 0; k < 12; k++) a.l[k] = __builtin_amdgcn_raw_buffer_load_b32(r, vo, soa_word_off(n, k), 0);
+  return a;
+}
+#endif
+DI void st_fp2_v(uint32_t* buf, size_t n, size_t i, int slot, const fp2& a) {
+  st_fp_v(buf, n, i, slot, a.c0);
+  st_fp_v(buf, n, i, slot + 1, a.c1);
+}
+DI fp2 ld_fp2_v(const uint32_t* buf, size_t n, size_t i, int slot) {
+  return {ld_fp_v(buf, n, i, slot), ld_fp_v(buf, n, i, slot + 1)};
 }
 
 DI void st_fp2(uint32_t* buf, size_t n, size_t i, int slot, const fp2& a) {

@@ -137,11 +137,11 @@ DI int tri_slot_a(unsigned role) { return role == 0 ? 0 : (role == 1 ? 6 : 2); }
 DI int tri_slot_b(unsigned role) { return role == 0 ? 8 : (role == 1 ? 4 : 10); }
 
 DI fp4 tri_load(const uint32_t* buf, size_t n, size_t i, unsigned role) {
-  return {ld_fp2(buf, n, i, tri_slot_a(role)), ld_fp2(buf, n, i, tri_slot_b(role))};
+  return {ld_fp2_v(buf, n, i, tri_slot_a(role)), ld_fp2_v(buf, n, i, tri_slot_b(role))};
 }
 DI void tri_store(uint32_t* buf, size_t n, size_t i, unsigned role, const fp4& x) {
-  st_fp2(buf, n, i, tri_slot_a(role), x.a);
-  st_fp2(buf, n, i, tri_slot_b(role), x.b);
+  st_fp2_v(buf, n, i, tri_slot_a(role), x.a);
+  st_fp2_v(buf, n, i, tri_slot_b(role), x.b);
 }
 
 // ------------------------------------------------------------------ Fp12 operations on thirds

@@ -186,9 +186,13 @@ WVI bool hash_to_g2(const uint32_t (&b0)[8], F& hx, F& hy) {
   xmd_words(b0, e);
   const F u[2] = {fp2_from_be512(e[0], e[1]), fp2_from_be512(e[2], e[3])};
   F x[2], y[2];
+  WV_MARK(10);
   sswu2(u, x, y);
+  WV_MARK(11);
   const G2J q = g2_add(iso_map(x[0], y[0]), iso_map(x[1], y[1]));
+  WV_MARK(12);
   const G2J h = g2_clear_cofactor(q);
+  WV_MARK(13);
   if (g2_is_inf(h)) return false;
   g2_to_affine(h, hx, hy);
   return true;
@@ -259,6 +263,7 @@ WVI uint8_t g2_decompress(const uint8_t* in, F& ox, F& oy, bool& is_inf) {
   const uint64_t nz = ballot(((l & 16u) == 0u) & (yr != 0u));
   const bool largest = half_bits(nz, 1) != 0 ? ((gt >> 1) & 1u) != 0 : (gt & 1u) != 0;
   if (largest != sign) y = mul2(y, cst(WC_NEG1));  // -y, reduced (a later subtrahend)
+  WV_MARK(14);
   if (!g2_in_subgroup({x, y, cst(WC_ONE2)})) return bls::REJ_NOT_IN_SUBGROUP;
   ox = x;
   oy = y;

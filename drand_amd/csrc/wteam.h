@@ -27,19 +27,6 @@ constexpr int BLK_SLOTS = WV_BLK_SLOTS;
 constexpr int BLK_CTRS = 8;   // team counters
 constexpr int BLK_WORDS_EXTRA = 64;  // scalar words (verdicts, flags)
 
-// Phase trace of the latency kernel (blsv_lat_trace): wave-lane 0 of item 0 (block 0) stamps the
-// device wall clock at the marks of wvteam.h verify_team; a no-op in every other block and on the host.
-constexpr int LAT_TRACE_N = 16;
-#ifdef WV_HOST
-#define WV_MARK(k) ((void)0)
-#else
-extern __device__ uint64_t g_lat_trace[LAT_TRACE_N];
-#define WV_MARK(k)                                                                     \
-  do {                                                                                 \
-    if (blockIdx.x == 0 && (threadIdx.x & 63u) == 0u) g_lat_trace[(k)] = wall_clock64(); \
-  } while (0)
-#endif
-
 #ifdef WV_HOST
 extern uint32_t g_host_blk[BLK_SLOTS * 64 + BLK_WORDS_EXTRA];
 extern double g_host_blk_b[BLK_SLOTS];

@@ -304,7 +304,8 @@ class Engine:
         return {s: (ms[k], la[k], it[k]) for k, s in enumerate(self.STAGES)}
 
     LAT_MARKS = ("start", "hash", "sig_decoded", "sig_miller", "phase_a", "key_miller", "miller_product",
-                 "final_exp", "pow1_start", "pow1_end")
+                 "final_exp", "pow1_start", "pow1_end", "xmd_done", "sswu_done", "iso_add_done", "cofactor_done",
+                 "sig_sqrt_done")
 
     def lat_trace(self, clear=True):
         """Phase marks (microseconds from the first mark) of item 0 of the last latency-path launch

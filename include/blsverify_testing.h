@@ -45,7 +45,9 @@ int blsv_profile_enable(blsv_ctx* ctx, int on);
  * Phase marks of the latency path (k_lat.hip): item 0 of the last latency launch stamps the device
  * wall clock at up to 16 marks of wvteam.h verify_team (0 start, 1 hash done, 2 signature decoded,
  * 3 signature pair's Miller loop done, 4 phase A joined, 5 key pair's Miller loop done, 6 Miller
- * product ready, 7 final exponentiation done, 8/9 first exponentiation by |x| start/end). Copies n
+ * product ready, 7 final exponentiation done, 8/9 first exponentiation by |x| start/end, 10-13 hash:
+ * xmd done, both SSWU maps done, isogeny + addition done, cofactor cleared, 14 signature's square
+ * root done (before its subgroup check)). Copies n
  * marks (0 = never stamped) into ticks, the clock rate into *ticks_per_us, and zeroes the marks when
  * clear != 0. Returns the number of marks copied.
  */
