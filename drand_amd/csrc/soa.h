@@ -6,11 +6,8 @@
 
 namespace bls {
 
-#ifndef BLS_SOA_BUF
-#define BLS_SOA_BUF 0
-#endif
 
-#if defined(BLS_HOST) || !BLS_SOA_BUF
+#ifdef BLS_HOST
 DI void st_fp(uint32_t* buf, size_t n, size_t i, int slot, const fp& a) {
 #pragma unroll
   for (int k = 0; k < 12; k++) buf[(size_t)(slot * 12 + k) * n + i] = a.l[k];
@@ -23,10 +20,13 @@ DI fp ld_fp(const uint32_t* buf, size_t n, size_t i, int slot) {
   return a;
 }
 #else
-// Buffer-resource form: the slot's 12 words are one resource (base = the slot's first column, at
-// most 12 n words), the item's byte offset i * 4 is the one VGPR offset and each word's k * n * 4 an
-// SGPR offset recomputed at its use (an opaque stride keeps LLVM from hoisting a kernel's hundreds
-// of distinct offsets into SGPRs it then spills) -- no 64-bit VGPR address per word.
+// Device form through buffer resources: the slot's 12 words are one resource (base = the slot's
+// first column, at most 12 n words), the item's byte offset i * 4 is the one VGPR offset and each
+// word's k * n * 4 an SGPR offset recomputed at its use (an opaque stride keeps LLVM from hoisting a
+// kernel's hundreds of distinct offsets into SGPRs it then spills) -- no 64-bit VGPR address per
+// word. Against plain global pointers (r04 A/B, profiles/r04i_soabuf_team_f_ab.json): scratch of the
+// 3-lane final exponentiation 480 -> 128 B/lane, cofactor clearing 1,884 -> 988, the 3-lane f pass
+// 1,328 -> 144; 2.100 -> 2.129 M beacons/s on one box. Loads past the resource return 0, never fault.
 DI __amdgpu_buffer_rsrc_t soa_slot_rsrc(const uint32_t* buf, size_t n, int slot) {
   const size_t bytes = (size_t)12 * n * 4;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(buf) + (size_t)slot * 12 * n, 0,
@@ -55,8 +55,8 @@ DI fp ld_fp(const uint32_t* buf, size_t n, size_t i, int slot) {
 // A lane-varying slot (the 3-lane layouts pick slots by lane role): the buffer form keeps ONE
 // resource over the whole object -- at most 12 Fp slots from `buf` (an Fp12, a line pair's six
 // slots) -- since a resource must be wave-uniform, and moves the slot into the VGPR offset; the
-// plain form is the same as st_fp / ld_fp.
-#if defined(BLS_HOST) || !BLS_SOA_BUF
+// host form is the same as st_fp / ld_fp.
+#ifdef BLS_HOST
 DI void st_fp_v(uint32_t* buf, size_t n, size_t i, int slot, const fp& a) { st_fp(buf, n, i, slot, a); }
 DI fp ld_fp_v(const uint32_t* buf, size_t n, size_t i, int slot) { return ld_fp(buf, n, i, slot); }
 #else
