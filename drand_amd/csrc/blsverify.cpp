@@ -19,10 +19,10 @@
 namespace {
 
 constexpr size_t kMaxChunk = size_t(1) << 20;  // beacons per pipeline pass (~1 GB of staging)
-#ifndef BLS_LINE_SUB_LOG2
-#define BLS_LINE_SUB_LOG2 17
-#endif
-constexpr size_t kLineSub = size_t(1) << BLS_LINE_SUB_LOG2;  // Miller line staging: 128 Ki beacons x 39 KB = 5.1 GB
+// Miller line staging holds a whole chunk: 1 Mi beacons x 39 KB = 41 GB of the 288 GB. Same-box A/B
+// (profiles/r04k_line_sub_ab.json): 128 Ki sub-chunks 216.9 ms, 256 Ki 215.8, the whole chunk 210.7 per 1M
+// (one lines + one f launch instead of eight of each, so one wave tail instead of eight).
+constexpr size_t kLineSub = kMaxChunk;
 
 struct DBuf {
   void* p = nullptr;

@@ -254,7 +254,8 @@ BLS_KERNEL(BLS_WPE_MILLER_TRI) k_miller_f_tri(const uint32_t* LN, const uint8_t*
 }
 
 // ------------------------------------------------------------------ launchers
-// The line staging (MILLER_LINE_WORDS per beacon) holds `sub` beacons; the chunk runs in sub-chunks.
+// The line staging (MILLER_LINE_WORDS per beacon) holds `sub` beacons; the chunk runs in sub-chunks
+// (one when sub >= cnt, which is what the host does: every sub-chunk adds a wave tail to both passes).
 void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
                    const uint8_t* h_inf, const uint32_t* S, const uint8_t* s_inf, const uint8_t* cls, size_t cnt,
                    uint32_t* F, uint32_t* LN, size_t sub, uint32_t* park, hipStream_t st) {

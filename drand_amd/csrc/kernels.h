@@ -46,7 +46,8 @@ void launch_hash_messages(const uint8_t* msgs, const uint64_t* off, const uint32
 void launch_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, size_t base, size_t cnt, uint32_t* S,
                           uint8_t* s_inf, uint8_t* cls, hipStream_t st);
 // pk for item i: pk_tab[pk_idx ? pk_idx[i] : 0] (G1_WORDS each) with pk_inf flags
-// LN: line staging for `sub` beacons (MILLER_LINE_WORDS each); the chunk runs in sub-chunks
+// LN: line staging for `sub` beacons (MILLER_LINE_WORDS each); the chunk runs in sub-chunks of `sub`
+// (the host passes the whole chunk: blsverify.cpp kLineSub)
 constexpr int MILLER_LINE_WORDS = 68 * 2 * 6 * 12;
 void launch_miller(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk_idx, const uint32_t* H,
                    const uint8_t* h_inf, const uint32_t* S, const uint8_t* s_inf, const uint8_t* cls, size_t cnt,
