@@ -1,14 +1,15 @@
-// Latency path: one workgroup of four waves verifies one item end to end (wvteam.h: limbs across
+// Latency path: one workgroup of eight waves verifies one item end to end (wvteam.h: limbs across
 // lanes, the item's independent work across the waves). Used for small batches (blsverify.cpp routes
 // batches up to BLSV_LAT_MAX items here), where the batch pipeline's one-lane-per-item stages would
 // leave the chip idle and pay a serial chain of ~16 M VALU instructions per lane. Same inputs and
 // reject classes as the batch stages; the verdicts then go through launch_finish like theirs.
-#define WV_WAVES 4
+#define WV_WAVES 8
 #include "kcommon.h"
 #include "wvteam.h"
 
 namespace wv {
 __device__ uint64_t g_lat_trace[LAT_TRACE_N];
+static_assert(TEAM_WAVES == WV_WAVES, "one wave of the workgroup per team member");
 }
 
 namespace blsk {
@@ -53,7 +54,7 @@ DI void lat_verify(MsgB0 msg_b0, size_t i, const uint8_t* sig, const uint32_t* p
   if (S && (c == REJ_OK || c == REJ_PAIRING)) store_sigma(S, s_inf, s_n, i, sx, sy, sinf);
 }
 
-__global__ void __launch_bounds__(256) k_lat_chained(ChainedSrc src, size_t base, size_t cnt, const uint32_t* pk_tab,
+__global__ void __launch_bounds__(64 * WV_WAVES) k_lat_chained(ChainedSrc src, size_t base, size_t cnt, const uint32_t* pk_tab,
                                                     const uint8_t* pk_inf, uint8_t* cls) {
   const size_t i = blockIdx.x;
   if (i >= cnt) return;
@@ -71,7 +72,7 @@ __global__ void __launch_bounds__(256) k_lat_chained(ChainedSrc src, size_t base
       i, src.sigs + g * 96, pk_tab, pk_inf, nullptr, cls, nullptr, nullptr, 0);
 }
 
-__global__ void __launch_bounds__(256) k_lat_unchained(const uint64_t* rounds, uint64_t first_round, const uint8_t* sigs,
+__global__ void __launch_bounds__(64 * WV_WAVES) k_lat_unchained(const uint64_t* rounds, uint64_t first_round, const uint8_t* sigs,
                                                       size_t base, size_t cnt, const uint32_t* pk_tab,
                                                       const uint8_t* pk_inf, uint8_t* cls) {
   const size_t i = blockIdx.x;
@@ -85,7 +86,7 @@ __global__ void __launch_bounds__(256) k_lat_unchained(const uint64_t* rounds, u
       i, sigs + (base + i) * 96, pk_tab, pk_inf, nullptr, cls, nullptr, nullptr, 0);
 }
 
-__global__ void __launch_bounds__(256) k_lat_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len,
+__global__ void __launch_bounds__(64 * WV_WAVES) k_lat_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len,
                                                      const uint8_t* sigs, size_t stride, size_t offset, size_t cnt,
                                                      const uint32_t* pk_tab, const uint8_t* pk_inf,
                                                      const uint32_t* pk_idx, uint8_t* cls, uint32_t* S,
@@ -114,19 +115,19 @@ int lat_trace_clear(hipStream_t st) {
 
 void launch_lat_chained(const ChainedSrc& src, size_t base, size_t cnt, const uint32_t* pk_tab, const uint8_t* pk_inf,
                         uint8_t* cls, hipStream_t st) {
-  if (cnt) hipLaunchKernelGGL(k_lat_chained, dim3((unsigned)cnt), dim3(256), 0, st, src, base, cnt, pk_tab, pk_inf, cls);
+  if (cnt) hipLaunchKernelGGL(k_lat_chained, dim3((unsigned)cnt), dim3(64 * WV_WAVES), 0, st, src, base, cnt, pk_tab, pk_inf, cls);
 }
 void launch_lat_unchained(const uint64_t* rounds, uint64_t first_round, const uint8_t* sigs, size_t base, size_t cnt,
                           const uint32_t* pk_tab, const uint8_t* pk_inf, uint8_t* cls, hipStream_t st) {
   if (cnt)
-    hipLaunchKernelGGL(k_lat_unchained, dim3((unsigned)cnt), dim3(256), 0, st, rounds, first_round, sigs, base, cnt,
+    hipLaunchKernelGGL(k_lat_unchained, dim3((unsigned)cnt), dim3(64 * WV_WAVES), 0, st, rounds, first_round, sigs, base, cnt,
                        pk_tab, pk_inf, cls);
 }
 void launch_lat_messages(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, const uint8_t* sigs,
                          size_t stride, size_t offset, size_t cnt, const uint32_t* pk_tab, const uint8_t* pk_inf,
                          const uint32_t* pk_idx, uint8_t* cls, uint32_t* S, uint8_t* s_inf, hipStream_t st) {
   if (cnt)
-    hipLaunchKernelGGL(k_lat_messages, dim3((unsigned)cnt), dim3(256), 0, st, msgs, off, len, sigs, stride, offset, cnt,
+    hipLaunchKernelGGL(k_lat_messages, dim3((unsigned)cnt), dim3(64 * WV_WAVES), 0, st, msgs, off, len, sigs, stride, offset, cnt,
                        pk_tab, pk_inf, pk_idx, cls, S, s_inf);
 }
 

@@ -569,6 +569,13 @@ WVI F inv_pair(const F& a, bool both = true) {
   // the GCD's output is < 2p: as a product operand it is a value below 2p
   return mulp(mkF(words_to_limbs(w0, w1), 2.0), cst(WC_C416_DUP));
 }
+// per half: a_h^-1 for two NONZERO halves, one GCD (Montgomery's trick): 1 / (a0 a1) times the
+// other half
+WVI F inv_pair_nz(const F& a) {
+  const F other = swap_halves(a);
+  const F ni = inv_pair(mulp(a, other), false);
+  return mulp(ni, other);
+}
 WVI F inv_pair_pow(const F& a) { return pow_pair<12>(a, bls::EXP_P_MINUS_2); }  // 0 -> 0
 WVI F pow_pm3d4(const F& a) { return pow_pair<12>(a, bls::EXP_P_MINUS_3_DIV_4); }  // sqrt and its inverse
 WVI F inv2(const F& a) {  // Fp2: conj(a) / N(a) (the norm is duplicated: one GCD)

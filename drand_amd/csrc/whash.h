@@ -118,7 +118,7 @@ WVI void sswu2(const F (&u)[2], F (&xo)[2], F (&yo)[2]) {
   // tv1 = inv0(den) = conj(den) / N(den): the two norms inverted as one pair
   const F nd = select_halves(1u, norm_dup(den[0]), norm_dup(den[1]));
   dz = zero_halves(nd);
-  const F ndi = inv_pair(select_halves(dz, cst(WC_ONE_DUP), nd));
+  const F ndi = inv_pair_nz(select_halves(dz, cst(WC_ONE_DUP), nd));  // zero norms replaced by 1
   F gx1[2], x1[2];
   for (int m = 0; m < 2; m++) {
     const bool z = (dz >> m) & 1u;
@@ -180,8 +180,8 @@ WVI G2J iso_map(const F& x, const F& y) {
   return {X, Y, Z};  // Z == 0 (the isogeny's kernel) is the point at infinity
 }
 
-// H(msg) affine from the message's xmd b_0; returns false for the point at infinity (inactive pair)
-WVI bool hash_to_g2(const uint32_t (&b0)[8], F& hx, F& hy) {
+// the sum of the two mapped points (before the cofactor clearing) from the message's xmd b_0
+WVI G2J hash_to_curve_sum(const uint32_t (&b0)[8]) {
   uint32_t e[4][16];
   xmd_words(b0, e);
   const F u[2] = {fp2_from_be512(e[0], e[1]), fp2_from_be512(e[2], e[3])};
@@ -191,7 +191,12 @@ WVI bool hash_to_g2(const uint32_t (&b0)[8], F& hx, F& hy) {
   WV_MARK(11);
   const G2J q = g2_add(iso_map(x[0], y[0]), iso_map(x[1], y[1]));
   WV_MARK(12);
-  const G2J h = g2_clear_cofactor(q);
+  return q;
+}
+
+// H(msg) affine from the message's xmd b_0; returns false for the point at infinity (inactive pair)
+WVI bool hash_to_g2(const uint32_t (&b0)[8], F& hx, F& hy) {
+  const G2J h = g2_clear_cofactor(hash_to_curve_sum(b0));
   WV_MARK(13);
   if (g2_is_inf(h)) return false;
   g2_to_affine(h, hx, hy);
@@ -199,8 +204,10 @@ WVI bool hash_to_g2(const uint32_t (&b0)[8], F& hx, F& hy) {
 }
 
 // ------------------------------------------------------------------ G2 decompression
-// 96-byte compressed point (wave-uniform bytes) -> affine (x, y), kilic FromCompressed check order
-WVI uint8_t g2_decompress(const uint8_t* in, F& ox, F& oy, bool& is_inf) {
+// 96-byte compressed point (wave-uniform bytes) -> affine (x, y), kilic FromCompressed check order;
+// with subgroup = false the final subgroup check is left to the caller (wvteam.h runs it beside the
+// signature's Miller loop)
+WVI uint8_t g2_decompress(const uint8_t* in, F& ox, F& oy, bool& is_inf, bool subgroup = true) {
   is_inf = false;
   const uint8_t b0 = in[0];
   if (!(b0 & 0x80)) return bls::REJ_FLAG;
@@ -264,7 +271,7 @@ WVI uint8_t g2_decompress(const uint8_t* in, F& ox, F& oy, bool& is_inf) {
   const bool largest = half_bits(nz, 1) != 0 ? ((gt >> 1) & 1u) != 0 : (gt & 1u) != 0;
   if (largest != sign) y = mul2(y, cst(WC_NEG1));  // -y, reduced (a later subtrahend)
   WV_MARK(14);
-  if (!g2_in_subgroup({x, y, cst(WC_ONE2)})) return bls::REJ_NOT_IN_SUBGROUP;
+  if (subgroup && !g2_in_subgroup({x, y, cst(WC_ONE2)})) return bls::REJ_NOT_IN_SUBGROUP;
   ox = x;
   oy = y;
   return bls::REJ_OK;

@@ -8,7 +8,8 @@
 
 namespace wv {
 
-// one Miller pair: G1 point P as Fp scalars duplicated over both halves, Q affine on the twist
+// one Miller pair: G1 point P as Fp scalars duplicated over both halves, Q on the twist (affine, or
+// homogeneous projective (qx : qy : qz) for the team loop, wvteam.h)
 struct MPair {
   F xp3;   // 3 xP        (doubling line l01 = 3 X^2 xP)
   F m2yp;  // -2 yP       (doubling line l11 = -H yP = -2 Y Z yP)
@@ -16,6 +17,8 @@ struct MPair {
   F yp;    // yP          (addition line l11)
   F qx, qy, mqx, mqy;  // Q and -Q's coordinates
   G2J t;   // running T = [k] Q
+  bool qaff = true;    // qz == 1
+  F qz, mxpz, ypz;     // projective Q only: qz, -xP qz, yP qz
 };
 
 WVI MPair mpair(const F& xp, const F& yp, const F& qx, const F& qy) {
@@ -29,6 +32,18 @@ WVI MPair mpair(const F& xp, const F& yp, const F& qx, const F& qy) {
   m.mqx = neg<0>(qx);
   m.mqy = neg<0>(qy);
   m.t = {qx, qy, cst(WC_ONE2)};
+  return m;
+}
+
+// Q = (qx : qy : qz) homogeneous: the addition lines come out scaled by qz^2, an Fp2 factor that the
+// final exponentiation removes (every element of a proper subfield has order dividing p^6 - 1)
+WVI MPair mpair_proj(const F& xp, const F& yp, const F& qx, const F& qy, const F& qz) {
+  MPair m = mpair(xp, yp, qx, qy);
+  m.t.z = qz;
+  m.qaff = false;
+  m.qz = qz;
+  m.mxpz = mulp(qz, m.mxp);
+  m.ypz = mulp(qz, yp);
   return m;
 }
 

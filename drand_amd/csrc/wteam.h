@@ -71,11 +71,15 @@ WVI uint32_t xld_word(int i) {
 }
 
 struct Team {
-  int first, n, id;  // waves first .. first + n - 1; this wave's index in the team
-  int ctr;           // its counter
-  uint32_t gen;      // syncs passed
+  int n, id;     // members; this wave's index among them (waves in increasing order)
+  int ctr;       // its counter
+  uint32_t gen;  // syncs passed
 };
-WVI Team make_team(int first, int n, int ctr) { return {first, n, wave_id() - first, ctr, 0u}; }
+// the waves of `mask` (bit w = wave w); only members may call team_sync
+WVI Team make_team(uint32_t mask, int ctr) {
+  const uint32_t below = mask & ((1u << wave_id()) - 1u);
+  return {__builtin_popcount(mask), __builtin_popcount(below), ctr, 0u};
+}
 
 WVI void team_sync(Team& t) {
   t.gen++;
@@ -93,6 +97,36 @@ WVI void team_sync(Team& t) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #endif
 }
+
+// one-shot hand-off between waves outside a common team: the producer posts after its LDS stores,
+// consumers wait for `count` posts
+WVI void flag_post(int ctr) {
+#ifdef WV_HOST
+  g_host_ctr[ctr].fetch_add(1, std::memory_order_acq_rel);
+#else
+  uint32_t* c = blk_base() + BLK_SLOTS * 64 + BLK_WORDS_EXTRA + ctr;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (threadIdx.x % 64 == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+}
+WVI void flag_wait(int ctr, uint32_t count) {
+#ifdef WV_HOST
+  while (g_host_ctr[ctr].load(std::memory_order_acquire) < count) std::this_thread::yield();
+#else
+  uint32_t* c = blk_base() + BLK_SLOTS * 64 + BLK_WORDS_EXTRA + ctr;
+  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < count)
+    __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#endif
+}
+
+// issue priority of the calling wave among the waves of its SIMD (0 .. 3; the critical path's wave
+// runs above the wave that shares its SIMD)
+#ifdef WV_HOST
+#define WV_PRIO(p) ((void)0)
+#else
+#define WV_PRIO(p) __builtin_amdgcn_s_setprio(p)
+#endif
 
 // the workgroup prologue: counters to zero (then a workgroup barrier before any team sync)
 WVI void team_init() {

@@ -1,38 +1,58 @@
-// One verification by a team of four waves (one per SIMD of a CU), the latency engine's device form
+// One verification by a team of eight waves (two per SIMD of a CU), the latency engine's device form
 // (k_lat.hip). The work of wverify.h's verify_item, scheduled across the waves:
 //
-//   phase A  wave 0: hash-to-G2 of the message            waves 1-3: decompress + subgroup check of
-//                                                          the signature (wave 1), then the Miller
-//                                                          loop of the signature pair (e(-g1, S)),
-//                                                          as a team of three
-//   phase B  all four: the Miller loop of the key pair (e(pk, H(m)))
-//   phase C  all four: the product of the two Miller values and the final exponentiation
+//   phase A  wave 0: hash-to-G2 of the message at raised issue priority; waves 4, 5 join it for the
+//            cofactor clearing (team_clear_cofactor: each doubling in three rounds)
+//            wave 1: decompression of the signature, then its subgroup check
+//            waves 2, 3, 6, 7: as soon as wave 1 has the point, the Miller loop of the signature
+//            pair (e(-g1, S)) -- the subgroup check runs beside it, its verdict joins at the end
+//   phase B  all eight: the Miller loop of the key pair (e(pk, H(m)))
+//   phase C  all eight: the product of the two Miller values and the final exponentiation
 //
 // The two Miller loops run separately (f = f_0 f_1 with each f_k its own loop's product: squaring
 // is multiplicative), so the signature's pair needs no hash and overlaps it. A Miller doubling step
-// is two team rounds: (1) the six coefficients of f^2 two per wave beside the line pieces (A, X^2 ->
-// l2, YZ -> l3, and B, C, E -> l0 with T's new Z on the fourth wave); (2) f^2 times the line two
-// coefficients per wave while the fourth wave finishes T. Every Fp12 operation of the final
-// exponentiation splits its six output coefficients two per wave over three waves.
+// is two team rounds of jobs (dbl_job1 / dbl_job2): (1) the six coefficients of f^2 and the line and
+// T pieces (X^2 -> l2, Z^2 -> E, YZ -> l3, A, B), (2) the six coefficients of f^2 l and T's new X, Y,
+// Z; an addition step is four rounds of one-product jobs. Every Fp12 operation of the final
+// exponentiation gives its six output coefficients to six waves. Two waves per SIMD each run at ~0.8
+// of a lone wave's pace (profiles/r04m_latency_sweep.json: 512 teams of four on 256 CUs take 1.21x
+// the time of 256), so halving the rounds of a step pays.
 #pragma once
 #include "wteam.h"
 #include "wverify.h"
 
 namespace wv {
 
+constexpr int TEAM_WAVES = 8;
+constexpr uint32_t ALL_WAVES = 0xFFu;
+constexpr uint32_t SIG_TEAM = (1u << 2) | (1u << 3) | (1u << 6) | (1u << 7);
+constexpr uint32_t HASH_TEAM = (1u << 0) | (1u << 4) | (1u << 5);
+
 // ------------------------------------------------------------------ block LDS slots (wteam.h)
-// team areas (one per Miller loop): f double buffer, f^2, T, line, step intermediates
+// team areas (one per Miller loop): f double buffer, f^2, T, lines, step intermediates
 constexpr int TA_FB = 0, TA_FSQ = 12, TA_TX = 18, TA_TY = 19, TA_TZ = 20, TA_L0 = 21, TA_L2 = 22, TA_L3 = 23,
-              TA_A = 24, TA_B = 25, TA_E = 26, TA_G = 27, TA_ZN = 28, TA_SIZE = 32;
+              TA_A = 24, TA_B = 25, TA_E = 26, TA_YZ = 27, TA_TH = 28, TA_DL = 29, TA_AF = 30, TA_AG = 31,
+              TA_SIZE = 32;
+// the addition step's C, D, E reuse the doubling's A, B, E slots, its X qz, Y qz, Z qz those of f^2
+// (free between the doubling's round 2 and the next doubling's round 1)
+constexpr int TA_AC = TA_A, TA_AD = TA_B, TA_AE = TA_E, TA_QX = TA_FSQ, TA_QY = TA_FSQ + 1, TA_QZ = TA_FSQ + 2;
 constexpr int TB0 = 0, TB1 = TA_SIZE;  // key pair, signature pair
 // final exponentiation values (6 slots each)
 constexpr int W_BASE = 2 * TA_SIZE;
 constexpr int W_R = W_BASE, W_INV = W_BASE + 6, W_T = W_BASE + 12, W_U = W_BASE + 18, W_G = W_BASE + 24,
               W_P = W_BASE + 30, W_S = W_BASE + 36, W_A = W_BASE + 42, W_B = W_BASE + 48, W_C = W_BASE + 54;
 constexpr int S_HX = W_BASE + 60, S_HY = S_HX + 1, S_SX = S_HX + 2, S_SY = S_HX + 3;
+// H's homogeneous Z: the key area's last slot (written in phase A after the hash team's slots
+// TB0 .. TB0 + 13, read into the key pair before its loop first writes TA_AG)
+constexpr int S_HZ = TB0 + TA_AG;
 static_assert(S_SY < BLK_SLOTS, "block slots");
 // scalar words
-constexpr int XW_CLS = 0, XW_SINF = 1, XW_HFIN = 2, XW_F1 = 3;
+constexpr int XW_CLS = 0, XW_SINF = 1, XW_HFIN = 2, XW_F1 = 3, XW_SUB = 4, XW_ONE = 8;  // XW_ONE .. +5
+// counters: 0 all waves, 1 the signature team, 2 the decoded signature's hand-off, 3 the hash team
+constexpr int CTR_ALL = 0, CTR_SIG = 1, CTR_DEC = 2, CTR_HASH = 3;
+// the hash team's slots during phase A: the key pair's area (free until phase B)
+constexpr int HS_P = TB0, HS_ACC = TB0 + 3, HS_A = TB0 + 6, HS_B = TB0 + 7, HS_C = TB0 + 8, HS_D = TB0 + 9,
+              HS_EE = TB0 + 10, HS_Q2 = TB0 + 11;
 
 WVI W12 xld_w12(int base, bool cj = false) {
   W12 r;
@@ -46,76 +66,199 @@ WVI void xst_w12(int base, const W12& v) {
   for (int k = 0; k < 6; k++) xst(base + k, v.c[k]);
 }
 
-// output k of a six-output operation is computed by wave k / 2 of the team (a fourth wave idles)
+// output k of a six-output operation is computed by wave k of the team
 template <class Fn>
 WVI void team_op(Team& t, int dst, Fn fn) {
-  for (int k = 2 * t.id; k < 6 && k < 2 * t.id + 2; k++) xst(dst + k, fn(k));
+  for (int k = t.id; k < 6; k += t.n) xst(dst + k, fn(k));
   team_sync(t);
 }
 
-// ------------------------------------------------------------------ Miller loop of one pair
-// the four slots of a step run on waves s % n (a team of three doubles up slot 3 on wave 0)
-WVI void team_miller_dbl(Team& t, const MPair& m, int tb, int& cur) {
-  const int fin = tb + TA_FB + 6 * cur, fout = tb + TA_FB + 6 * (cur ^ 1);
-  for (int s = t.id; s < 4; s += t.n) {
-    if (s < 3) {
-      const W12 f = xld_w12(fin);
-      xst(tb + TA_FSQ + 2 * s, w12_sqr_c(f, 2 * s));
-      xst(tb + TA_FSQ + 2 * s + 1, w12_sqr_c(f, 2 * s + 1));
-      const F X = xld(tb + TA_TX), Y = xld(tb + TA_TY), Z = xld(tb + TA_TZ);
-      if (s == 0) xst(tb + TA_A, half(dot(X, Y)));          // X Y / 2
-      if (s == 1) xst(tb + TA_L2, mulp(sqr2(X), m.xp3));     // 3 X^2 xP
-      if (s == 2) xst(tb + TA_L3, mulp(dot(Y, Z), m.m2yp));  // -2 Y Z yP
-    } else {
-      const F Y = xld(tb + TA_TY), Z = xld(tb + TA_TZ);
-      const F B = sqr2(Y), C = sqr2(Z);
-      const F E = dot(C, cst(WC_B2X3));  // 3 b' Z^2
-      xst(tb + TA_L0, sub<0>(E, B));
-      xst(tb + TA_B, B);
-      xst(tb + TA_E, E);
-      xst(tb + TA_G, half(add(B, mul_small<3>(E))));  // (B + 3E) / 2
-      xst(tb + TA_ZN, dot(B, dbl(dot(Y, Z))));        // B H
-    }
+WVI void xst_g2(int base, const G2J& p) {
+  xst(base, p.x);
+  xst(base + 1, p.y);
+  xst(base + 2, p.z);
+}
+WVI G2J xld_g2(int base) { return {xld(base), xld(base + 1), xld(base + 2)}; }
+
+// ------------------------------------------------------------------ cofactor clearing by a team
+// wcurve.h g2_dbl (dbl-2009-l) in three rounds of one product per wave, on the accumulator's slots:
+// A = X^2, B = Y^2, Z3 = 2 Y Z | C = B^2, D = 4 X B, EE = (3A)^2 | X3 = E^2 - 2D, Y3 = E (3D - EE) - 8C
+// (Y3 = E (D - X3) - 8C with X3 substituted, so X3 and Y3 are one round)
+WVI void team_g2_dbl(Team& t, int acc) {
+  for (int j = t.id; j < 3; j += t.n) {
+    const F Y = xld(acc + 1);
+    if (j == 0) xst(HS_A, sqr2(xld(acc)));
+    else if (j == 1) xst(HS_B, sqr2(Y));
+    else xst(acc + 2, dot(dbl(Y), xld(acc + 2)));
   }
   team_sync(t);
-  for (int s = t.id; s < 4; s += t.n) {
-    if (s < 3) {
-      const W12 q = xld_w12(tb + TA_FSQ);
-      const F l0 = xld(tb + TA_L0), l2 = xld(tb + TA_L2), l3 = xld(tb + TA_L3);
-      xst(fout + 2 * s, w12_mul_line_c(q, l0, l2, l3, 2 * s));
-      xst(fout + 2 * s + 1, w12_mul_line_c(q, l0, l2, l3, 2 * s + 1));
-    } else {
-      const F A = xld(tb + TA_A), B = xld(tb + TA_B), E = xld(tb + TA_E), G = xld(tb + TA_G);
-      const F nE = neg<0>(E);
-      xst(tb + TA_TX, dot(A, B, mul_small<3>(A), nE));  // A (B - 3E)
-      xst(tb + TA_TY, dot(G, G, mul_small<3>(E), nE));  // G^2 - 3 E^2
-      xst(tb + TA_TZ, xld(tb + TA_ZN));
+  for (int j = t.id; j < 3; j += t.n) {
+    const F B = xld(HS_B);
+    if (j == 0) xst(HS_C, sqr2(B));
+    else if (j == 1) xst(HS_D, dot(xld(acc), mul_small<4>(B)));
+    else xst(HS_EE, sqr2(mul_small<3>(xld(HS_A))));
+  }
+  team_sync(t);
+  for (int j = t.id; j < 2; j += t.n) {
+    const F E = mul_small<3>(xld(HS_A)), D = xld(HS_D);
+    if (j == 0) xst(acc, dot(E, E, D, cst(WC_NEG2)));
+    else xst(acc + 1, dot(sub<0>(mul_small<3>(D), xld(HS_EE)), E, xld(HS_C), cst(WC_NEG8)));
+  }
+  team_sync(t);
+}
+// acc <- [|x|] acc (wcurve.h g2_mul_x_abs, acc == base on entry): the doublings by the team, the five
+// additions (with their exceptional cases) on its first wave
+WVI void team_mul_x_abs(Team& t, int base, int acc) {
+#pragma unroll 1
+  for (int i = 62; i >= 0; i--) {
+    team_g2_dbl(t, acc);
+    if ((bls::BLS_X_ABS >> i) & 1ull) {
+      if (t.id == 0) xst_g2(acc, g2_add(xld_g2(acc), xld_g2(base)));
+      team_sync(t);
     }
   }
+}
+// wcurve.h g2_clear_cofactor by the hash team: p is the first wave's (the others pass anything);
+// the result is the first wave's
+WVI G2J team_clear_cofactor(Team& t, const G2J& p) {
+  if (t.id == 0) {
+    xst_g2(HS_P, p);
+    xst_g2(HS_ACC, p);
+  }
+  team_sync(t);
+  team_mul_x_abs(t, HS_P, HS_ACC);
+  if (t.id == 0) {
+    const G2J a = g2_add(g2_neg(xld_g2(HS_ACC)), g2_psi(p));
+    xst_g2(HS_Q2, a);
+    xst_g2(HS_ACC, a);
+  }
+  team_sync(t);
+  team_mul_x_abs(t, HS_Q2, HS_ACC);
+  if (t.id != 0) return p;
+  G2J r = g2_add(g2_neg(xld_g2(HS_ACC)), g2_neg(xld_g2(HS_Q2)));
+  r = g2_add(r, g2_neg(p));
+  return g2_add(r, g2_psi2(g2_dbl(p)));
+}
+
+// ------------------------------------------------------------------ Miller loop of one pair
+// doubling round 1: 0..5 the coefficients of f^2, 6 X^2 -> l2 = 3 X^2 xP, 7 Z^2 -> E = 3 b' Z^2,
+// 8 YZ -> l3 = -2 Y Z yP, 9 A = X Y / 2, 10 B = Y^2 (pairing.h miller_dbl_step)
+WVI void dbl_job1(int j, const MPair& m, int tb, int fin) {
+  if (j < 6) {
+    xst(tb + TA_FSQ + j, w12_sqr_c(xld_w12(fin), j));
+    return;
+  }
+  const F X = xld(tb + TA_TX), Y = xld(tb + TA_TY), Z = xld(tb + TA_TZ);
+  switch (j) {
+    case 6: xst(tb + TA_L2, mulp(sqr2(X), m.xp3)); break;
+    case 7: xst(tb + TA_E, dot(sqr2(Z), cst(WC_B2X3))); break;
+    case 8: {
+      const F YZ = dot(Y, Z);
+      xst(tb + TA_YZ, YZ);
+      xst(tb + TA_L3, mulp(YZ, m.m2yp));
+      break;
+    }
+    case 9: xst(tb + TA_A, half(dot(X, Y))); break;
+    default: xst(tb + TA_B, sqr2(Y)); break;
+  }
+}
+// doubling round 2: 0..5 the coefficients of f^2 l (l0 = E - B), 6 X3 = A (B - 3E), 7 Y3 = G^2 - 3 E^2
+// with G = (B + 3E) / 2, 8 Z3 = B H with H = 2 Y Z
+WVI void dbl_job2(int j, int tb, int fout) {
+  const F B = xld(tb + TA_B), E = xld(tb + TA_E);
+  if (j < 6) {
+    const W12 q = xld_w12(tb + TA_FSQ);
+    xst(fout + j, w12_mul_line_c(q, sub<0>(E, B), xld(tb + TA_L2), xld(tb + TA_L3), j));
+    return;
+  }
+  const F nE = neg<0>(E);
+  if (j == 6) {
+    const F A = xld(tb + TA_A);
+    xst(tb + TA_TX, dot(A, B, mul_small<3>(A), nE));
+  } else if (j == 7) {
+    const F G = half(add(B, mul_small<3>(E)));
+    xst(tb + TA_TY, dot(G, G, mul_small<3>(E), nE));
+  } else {
+    xst(tb + TA_TZ, dot(B, dbl(xld(tb + TA_YZ))));
+  }
+}
+// round-1 jobs per wave (bit j = job j): jobs 6, 7, 8 are two products, the rest one
+WVI uint32_t dbl_jobs1(const Team& t) {
+  if (t.n == 8) {
+    constexpr uint16_t J8[8] = {(1 << 0) | (1 << 9), (1 << 1) | (1 << 10), (1 << 2) | (1 << 3), 1 << 8,
+                                1 << 4,              1 << 5,               1 << 6,              1 << 7};
+    return J8[t.id];
+  }
+  if (t.n == 5) {
+    constexpr uint16_t J5[5] = {(1 << 6) | (1 << 9), (1 << 7) | (1 << 10), (1 << 8) | (1 << 0),
+                                (1 << 1) | (1 << 2) | (1 << 3), (1 << 4) | (1 << 5)};
+    return J5[t.id];
+  }
+  uint32_t m = 0;
+  for (int j = t.id; j < 11; j += t.n) m |= 1u << j;
+  return m;
+}
+
+WVI void team_miller_dbl(Team& t, const MPair& m, int tb, int& cur) {
+  const int fin = tb + TA_FB + 6 * cur, fout = tb + TA_FB + 6 * (cur ^ 1);
+  const uint32_t jobs = dbl_jobs1(t);
+  for (int j = 0; j < 11; j++)
+    if ((jobs >> j) & 1u) dbl_job1(j, m, tb, fin);
+  team_sync(t);
+  for (int j = t.id; j < 9; j += t.n) dbl_job2(j, tb, fout);
   team_sync(t);
   cur ^= 1;
 }
 
+// addition step (pairing.h miller_add_step) in four rounds of one-product jobs. With a projective Q
+// (qx : qy : qz) it is the affine step with T's X, Y, Z replaced by X qz, Y qz, Z qz (those three are
+// extra round-1 jobs; theta, delta and the lines then carry a factor qz, qz^2):
+//   theta = Y qz - qy Z, delta = X qz - qx Z | l0, l2, l3, C = theta^2, D = delta^2 |
+//   f l, E = D delta, F = Zq C, G = Xq D | X3 = delta H, Y3 = theta (G - H) - Yq E, Z3 = Zq E,
+// H = E + F - 2G (Xq, Yq, Zq = X qz, Y qz, Z qz, or X, Y, Z for an affine Q)
 WVI void team_miller_add(Team& t, const MPair& m, int tb, int& cur) {
-  if (t.id == 3 % t.n) {
-    MPair mm = m;
-    mm.t = {xld(tb + TA_TX), xld(tb + TA_TY), xld(tb + TA_TZ)};
-    F l0, l2, l3;
-    miller_add(mm, l0, l2, l3);
-    xst(tb + TA_TX, mm.t.x);
-    xst(tb + TA_TY, mm.t.y);
-    xst(tb + TA_TZ, mm.t.z);
-    xst(tb + TA_L0, l0);
-    xst(tb + TA_L2, l2);
-    xst(tb + TA_L3, l3);
+  const int nj1 = m.qaff ? 2 : 5;
+  for (int j = t.id; j < nj1; j += t.n) {
+    const F Z = xld(tb + TA_TZ);
+    const F qz = m.qaff ? cst(WC_ONE2) : m.qz;
+    if (j == 0) xst(tb + TA_TH, dot(xld(tb + TA_TY), qz, Z, m.mqy));       // Y qz - qy Z
+    else if (j == 1) xst(tb + TA_DL, dot(xld(tb + TA_TX), qz, Z, m.mqx));  // X qz - qx Z
+    else if (j == 2) xst(tb + TA_QX, dot(xld(tb + TA_TX), qz));
+    else if (j == 3) xst(tb + TA_QY, dot(xld(tb + TA_TY), qz));
+    else xst(tb + TA_QZ, dot(Z, qz));
+  }
+  team_sync(t);
+  const int sx = m.qaff ? TA_TX : TA_QX, sy = m.qaff ? TA_TY : TA_QY, sz = m.qaff ? TA_TZ : TA_QZ;
+  for (int j = t.id; j < 5; j += t.n) {
+    const F theta = xld(tb + TA_TH), delta = xld(tb + TA_DL);
+    switch (j) {
+      case 0: xst(tb + TA_L0, dot(theta, m.qx, delta, m.mqy)); break;                        // theta qx - delta qy
+      case 1: xst(tb + TA_L2, m.qaff ? mulp(theta, m.mxp) : dot(theta, m.mxpz)); break;  // -theta xP (qz)
+      case 2: xst(tb + TA_L3, m.qaff ? mulp(delta, m.yp) : dot(delta, m.ypz)); break;    // delta yP (qz)
+      case 3: xst(tb + TA_AC, sqr2(theta)); break;
+      default: xst(tb + TA_AD, sqr2(delta)); break;
+    }
   }
   team_sync(t);
   const int fin = tb + TA_FB + 6 * cur, fout = tb + TA_FB + 6 * (cur ^ 1);
-  for (int s = t.id; s < 3; s += t.n) {
-    const W12 f = xld_w12(fin);
-    const F l0 = xld(tb + TA_L0), l2 = xld(tb + TA_L2), l3 = xld(tb + TA_L3);
-    xst(fout + 2 * s, w12_mul_line_c(f, l0, l2, l3, 2 * s));
-    xst(fout + 2 * s + 1, w12_mul_line_c(f, l0, l2, l3, 2 * s + 1));
+  for (int j = t.id; j < 9; j += t.n) {
+    if (j < 6) {
+      xst(fout + j, w12_mul_line_c(xld_w12(fin), xld(tb + TA_L0), xld(tb + TA_L2), xld(tb + TA_L3), j));
+    } else if (j == 6) {
+      xst(tb + TA_AE, dot(xld(tb + TA_AD), xld(tb + TA_DL)));
+    } else if (j == 7) {
+      xst(tb + TA_AF, dot(xld(tb + sz), xld(tb + TA_AC)));
+    } else {
+      xst(tb + TA_AG, dot(xld(tb + sx), xld(tb + TA_AD)));
+    }
+  }
+  team_sync(t);
+  for (int j = t.id; j < 3; j += t.n) {
+    const F E = xld(tb + TA_AE), G = xld(tb + TA_AG);
+    const F H = sub<0>(add(E, xld(tb + TA_AF)), dbl(G));  // E + F - 2G
+    if (j == 0) xst(tb + TA_TX, dot(xld(tb + TA_DL), H));
+    else if (j == 1) xst(tb + TA_TY, dot(xld(tb + TA_TH), sub<1>(G, H), xld(tb + sy), neg<0>(E)));
+    else xst(tb + TA_TZ, dot(xld(tb + sz), E));
   }
   team_sync(t);
   cur ^= 1;
@@ -188,41 +331,63 @@ WVI bool team_final_exp_is_one(Team& t, int f0) {
   team_op(t, W_U, [&](int k) { return w12_cyc_sqr_c(xld_w12(W_G), k); });
   team_op(t, W_P, [&](int k) { return w12_mul_c(xld_w12(W_A), xld_w12(W_U), k); });
   team_op(t, W_A, [&](int k) { return w12_mul_c(xld_w12(W_P), xld_w12(W_G), k); });
-  return w12_is_one(xld_w12(W_A));
+  // e == 1: coefficient k checked by wave k, the six verdicts through scalar words
+  for (int k = t.id; k < 6; k += t.n) {
+    const F c = xld(W_A + k);
+    xst_word(XW_ONE + k, is_zero2(k == 0 ? sub<0>(c, cst(WC_ONE2)) : c) ? 1u : 0u);
+  }
+  team_sync(t);
+  bool one = true;
+  for (int k = 0; k < 6; k++) one = one & (xld_word(XW_ONE + k) != 0u);
+  return one;
 }
 
 // ------------------------------------------------------------------ the item
-// wverify.h verify_item run by the four waves of a workgroup (each wave calls it); every wave returns
+// wverify.h verify_item run by the eight waves of a workgroup (each wave calls it); every wave returns
 // the same class, and sx, sy, s_inf (the decoded signature) on REJ_OK / REJ_PAIRING
 WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint32_t* pkx, const uint32_t* pky,
                         bool pk_inf, F& sx, F& sy, bool& s_inf) {
   const int w = wave_id();
-  Team all = make_team(0, 4, 0);
+  Team all = make_team(ALL_WAVES, CTR_ALL);
   if (w == 0) WV_MARK(0);
-  if (w == 0) {
-    F hx, hy;
-    const bool fin = hash_to_g2(b0, hx, hy);
-    WV_MARK(1);
-    if (fin) {
-      xst(S_HX, hx);
-      xst(S_HY, hy);
-    }
-    xst_word(XW_HFIN, fin);
-  } else {
-    Team t1 = make_team(1, 3, 1);
-    if (w == 1) {
-      F x, y;
-      bool inf;
-      const uint8_t c = g2_decompress(sig, x, y, inf);
-      WV_MARK(2);
-      if (c == bls::REJ_OK && !inf) {
-        xst(S_SX, x);
-        xst(S_SY, y);
+  if ((HASH_TEAM >> w) & 1u) {
+    // xmd, both SSWU maps and the isogeny on wave 0, the cofactor clearing by the hash team
+    Team th = make_team(HASH_TEAM, CTR_HASH);
+    WV_PRIO(2);  // above the signature branch's waves on SIMD 1 (wave 5) and the decoder (wave 1)
+    const G2J q = w == 0 ? hash_to_curve_sum(b0) : g2_infinity();
+    const G2J h = team_clear_cofactor(th, q);
+    if (w != 0) WV_PRIO(0);
+    if (w == 0) {
+      WV_MARK(13);
+      const bool fin = !g2_is_inf(h);
+      if (fin) {
+        // Jacobian (X, Y, Z) -> homogeneous (X Z : Y : Z^3): no inversion (mpair_proj)
+        xst(S_HX, dot(h.x, h.z));
+        xst(S_HY, h.y);
+        xst(S_HZ, dot(h.z, sqr2(h.z)));
       }
-      xst_word(XW_CLS, c);
-      xst_word(XW_SINF, inf);
+      WV_PRIO(0);
+      WV_MARK(1);
+      xst_word(XW_HFIN, fin);
     }
-    team_sync(t1);
+  } else if (w == 1) {
+    F x, y;
+    bool inf;
+    const uint8_t c = g2_decompress(sig, x, y, inf, false);
+    if (c == bls::REJ_OK && !inf) {
+      xst(S_SX, x);
+      xst(S_SY, y);
+    }
+    xst_word(XW_CLS, c);
+    xst_word(XW_SINF, inf);
+    flag_post(CTR_DEC);
+    WV_MARK(2);
+    const bool sub_ok = c != bls::REJ_OK || inf || g2_in_subgroup({x, y, cst(WC_ONE2)});
+    xst_word(XW_SUB, sub_ok);
+    WV_MARK(15);
+  } else if ((SIG_TEAM >> w) & 1u) {
+    Team t1 = make_team(SIG_TEAM, CTR_SIG);
+    flag_wait(CTR_DEC, 1);
     if (xld_word(XW_CLS) == bls::REJ_OK && !xld_word(XW_SINF)) {
       const MPair m1 = mpair(cst(WC_NEG_G1_X), cst(WC_NEG_G1_Y), xld(S_SX), xld(S_SY));
       const int f1 = team_miller(t1, m1, TB1);
@@ -232,7 +397,8 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
   }
   team_sync(all);
   if (w == 0) WV_MARK(4);
-  const uint8_t cls = (uint8_t)xld_word(XW_CLS);
+  uint8_t cls = (uint8_t)xld_word(XW_CLS);
+  if (cls == bls::REJ_OK && !xld_word(XW_SUB)) cls = bls::REJ_NOT_IN_SUBGROUP;
   if (cls != bls::REJ_OK) return cls;
   s_inf = xld_word(XW_SINF) != 0;
   if (!s_inf) {
@@ -243,7 +409,7 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
   if (!a0 && !a1) return bls::REJ_OK;  // empty product = 1 (kilic Check [ext])
   int f;
   if (a0) {
-    const MPair m0 = mpair(g1_coord(pkx), g1_coord(pky), xld(S_HX), xld(S_HY));
+    const MPair m0 = mpair_proj(g1_coord(pkx), g1_coord(pky), xld(S_HX), xld(S_HY), xld(S_HZ));
     f = team_miller(all, m0, TB0);
     if (w == 0) WV_MARK(5);
     if (a1) {

@@ -305,7 +305,7 @@ class Engine:
 
     LAT_MARKS = ("start", "hash", "sig_decoded", "sig_miller", "phase_a", "key_miller", "miller_product",
                  "final_exp", "pow1_start", "pow1_end", "xmd_done", "sswu_done", "iso_add_done", "cofactor_done",
-                 "sig_sqrt_done")
+                 "sig_sqrt_done", "sig_subgroup_done")
 
     def lat_trace(self, clear=True):
         """Phase marks (microseconds from the first mark) of item 0 of the last latency-path launch

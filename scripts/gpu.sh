@@ -12,8 +12,10 @@
 #   prof             rocprofv3 --kernel-trace --stats of bench.py with BLSV_SERIAL_STAGES=1
 #   pmc              PMC passes: FETCH_SIZE, WRITE_SIZE, two SQ/GRBM sets (tools/pmc_sq.py)
 #   cabi             tools/cabi_smoke (latency contract from plain C)
+#   wvbench          tools/wvbench (per-operation latency of the latency engine's primitives)
 #   intrate          tools/intrate (peak v_mad_u64_u32 rate) and its SQ/GRBM counters (clock of the peak)
-#   lat              tools/latency_bench.py (lone verify, fused round, crossover sweep)
+#   lat              tools/latency_bench.py (lone verify, fused round)
+#   latsweep         the same with the latency-vs-batch sweep (64 .. 2048 items: co-resident teams)
 #   cfg              tools/config_bench.py (configs[2], configs[4], partials, drand.db)
 #   variant:NAME     GPU suite + bench on variants/libblsverify_NAME.so (scripts/build_variant.sh,
 #                    loaded through DRAND_AMD_LIB)
@@ -65,7 +67,11 @@ for step in "$@"; do
         --output-format csv -d "$O/pmc_intrate" -o run -- tools/intrate > "$O/pmc_intrate.log" 2>&1 &&
       python3 tools/pmc_sq.py "$O/pmc_intrate.json" "$O/pmc_intrate/run_counter_collection.csv" > /dev/null || rc=23 ;;
     cabi) timeout -k 10 120 tools/cabi_smoke > "$O/cabi_smoke.txt" 2>&1 || rc=20 ;;
+    wvbench) timeout -k 10 120 tools/wvbench > "$O/wvbench.json" 2>&1 || rc=25 ;;
     lat) timeout -k 10 300 python -u tools/latency_bench.py --reps 10 --out "$O/latency.json" > "$O/latency.log" 2>&1 || rc=21 ;;
+    latsweep)
+      timeout -k 10 400 python -u tools/latency_bench.py --reps 5 --sweep 64,256,512,1024,2048 \
+        --out "$O/latency_sweep.json" > "$O/latency_sweep.log" 2>&1 || rc=24 ;;
     cfg) timeout -k 10 600 python -u tools/config_bench.py > "$O/config_bench.json" 2> "$O/config_bench.log" || rc=22 ;;
     variant:*)
       V=${step#variant:}

@@ -75,7 +75,7 @@ def test_decompress_matches_oracle(wvtest, golden):
 
 @pytest.mark.parametrize("cmd", ["verify", "tverify"])
 def test_verify_kat_and_chain(wvtest, golden, cmd):
-    """verify = one wave (wverify.h); tverify = the four-wave team of the device kernels (wvteam.h),
+    """verify = one wave (wverify.h); tverify = the eight-wave team of the device kernels (wvteam.h),
     one host thread per wave"""
     kat = golden["kat"]
     ch = golden["chained"]

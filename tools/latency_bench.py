@@ -116,13 +116,13 @@ def main():
             sweep = []
             for n in [int(x) for x in a.sweep.split(",")]:
                 msgs = [hashlib.sha256(b"sweep %d" % i).digest() for i in range(n)]
-                sigs = eng.sign(sk32, msgs)
+                msigs = eng.sign(sk32, msgs)
                 row = {"n": n}
                 for name, lm in (("lat_ms", 1 << 40), ("batch_ms", 0)):
                     eng.set_lat_max(lm)
 
                     def call():
-                        r = eng.verify_messages(msgs, sigs, pk48=pk)
+                        r = eng.verify_messages(msgs, msigs, pk48=pk)
                         assert all(r.ok)
 
                     row[name] = timed(call, 3)[0]

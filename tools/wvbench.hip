@@ -1,85 +1,101 @@
-// Latency / throughput microbenchmark of the latency engine's field products (drand_amd/csrc/
-// wfield.h) on MI355X: dependent chains of one product kind per wave, timed in-kernel with
-// s_memtime (one wave alone on the chip: the per-product latency a lone verification pays) and
-// with HIP events over growing grids (throughput when many items share the chip). The final value of
-// block 0 is printed so tools/wvbench_check.py can verify the chain against Python integers.
-// usage: wvbench [iters]
+// Per-operation latency of the latency engine's primitives (wfield.h / wteam.h) on an MI355X: one
+// workgroup of eight waves (the k_lat shape); an op runs `iters` times back to back on wave 0 alone
+// ("lone") or on waves 0..5 at once ("six": two waves share SIMDs 0 and 1, as in a team round), and
+// the device wall clock brackets the loop. Team modes time a whole team round (op + team_sync).
+//   hipcc --offload-arch=gfx950 -O3 -o wvbench wvbench.hip && ./wvbench
+#define WV_WAVES 8
 #include <hip/hip_runtime.h>
-#include <stdio.h>
-#include <stdlib.h>
+#include <cstdio>
+#include "../drand_amd/csrc/kcommon.h"
+#include "../drand_amd/csrc/wvteam.h"
 
-#include "../drand_amd/csrc/wverify.h"
-
+namespace wv {
+__device__ uint64_t g_lat_trace[LAT_TRACE_N];
+}
 using namespace wv;
 
-__global__ void __launch_bounds__(64) kchain(const uint32_t* in, uint32_t* out, int iters, int mode,
-                                             unsigned long long* cyc) {
-  wv_init();
-  F a = mkF(in[threadIdx.x], 1.0), b = mkF(in[64 + threadIdx.x], 1.0);
-  const unsigned long long t0 = __builtin_readcyclecounter();
-#pragma unroll 1
-  for (int i = 0; i < iters; i++) {
-    if (mode == 0) a = mul2(a, b);
-    else if (mode == 1) a = sqr2(a);
-    else if (mode == 2) a = mulp(a, b);
-    else if (mode == 3) a = dot(a, b, b, a, a, b, b, a, a, b, b, a);
-    else a = half(a);
-  }
-  const unsigned long long t1 = __builtin_readcyclecounter();
-  if (blockIdx.x == 0) out[threadIdx.x] = a.x;
-  if (blockIdx.x == 0 && threadIdx.x == 0) cyc[mode] = t1 - t0;
-}
+enum { OP_MULP, OP_DOT1, OP_DOT3, OP_DOT6, OP_SQR2, OP_INV2, OP_INV1, OP_ISZERO, OP_SYNC, OP_TEAM_CYC, OP_TEAM_MUL,
+       OP_N };
+static const char* NAMES[OP_N] = {"mulp", "dot1", "dot3", "dot6", "sqr2", "inv_pair2", "inv_pair1", "is_zero2",
+                                  "team_sync8", "team_cyc_sqr8", "team_mul8"};
 
-int main(int argc, char** argv) {
-  const int iters = argc > 1 ? atoi(argv[1]) : 2000;
-  // inputs: Montgomery-form values given as 25-bit limbs of two fixed integers (< p)
-  uint32_t h_in[128] = {0};
-  unsigned s = 12345;
-  for (int half = 0; half < 2; half++)
-    for (int k = 0; k < 15; k++) {
-      s = s * 1103515245u + 12345u;
-      h_in[32 * half + k] = (s >> 7) & ((1u << 25) - 1);
-      s = s * 1103515245u + 12345u;
-      h_in[64 + 32 * half + k] = (s >> 7) & ((1u << 25) - 1);
+__global__ void __launch_bounds__(512) k_wvbench(int op, int six, int iters, uint64_t* out) {
+  team_init();
+  wv_init();
+  __syncthreads();
+  const int w = wave_id();
+  F a = cst(WC_SSWU_Z), b = cst(WC_B2);
+  const bool team = op >= OP_SYNC;
+  const bool active = team || (six ? w < 6 : w == 0);
+  uint64_t t0 = 0, t1 = 0;
+  uint32_t keep = 0;
+  if (team) {
+    Team t = make_team(ALL_WAVES, CTR_ALL);
+    if (w == 0) {
+      W12 f;
+      for (int k = 0; k < 6; k++) f.c[k] = k & 1 ? a : b;
+      xst_w12(W_G, f);
+      xst_w12(W_S, f);
     }
-  printf("{\"inputs\": [");
-  for (int i = 0; i < 128; i++) printf("%u%s", h_in[i], i < 127 ? "," : "],\n");
-  uint32_t *d_in, *d_out;
-  unsigned long long* d_cyc;
-  hipMalloc(&d_in, sizeof h_in);
-  hipMalloc(&d_out, 64 * 4);
-  hipMalloc(&d_cyc, 8 * 8);
-  hipMemcpy(d_in, h_in, sizeof h_in, hipMemcpyHostToDevice);
-  hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
-  const char* names[] = {"mul2", "sqr2", "mulp", "dot6", "half"};
-  printf("\"iters\": %d, \"modes\": {", iters);
-  for (int mode = 0; mode < 5; mode++) {
-    printf("%s\"%s\": {", mode ? ", " : "", names[mode]);
-    const int grids[] = {1, 256, 1024, 4096};
-    for (int g = 0; g < 4; g++) {
-      hipLaunchKernelGGL(kchain, dim3(grids[g]), dim3(64), 0, 0, d_in, d_out, 10, mode, d_cyc);  // warm
-      hipEventRecord(e0, 0);
-      hipLaunchKernelGGL(kchain, dim3(grids[g]), dim3(64), 0, 0, d_in, d_out, iters, mode, d_cyc);
-      hipEventRecord(e1, 0);
-      hipEventSynchronize(e1);
-      float ms = 0;
-      hipEventElapsedTime(&ms, e0, e1);
-      unsigned long long cyc = 0;
-      hipMemcpy(&cyc, d_cyc + mode, 8, hipMemcpyDeviceToHost);
-      printf("%s\"grid%d\": {\"ms\": %.3f, \"us_per_op\": %.4f, \"ops_per_s\": %.4g, \"cycles_per_op_wave0\": %.1f}",
-             g ? ", " : "", grids[g], ms, ms * 1e3 / iters, (double)grids[g] * iters / (ms * 1e-3),
-             (double)cyc / iters);
-      if (g == 0) {
-        uint32_t h_out[64];
-        hipMemcpy(h_out, d_out, sizeof h_out, hipMemcpyDeviceToHost);
-        printf(", \"out\": [");
-        for (int i = 0; i < 64; i++) printf("%u%s", h_out[i], i < 63 ? "," : "]");
+    team_sync(t);
+    t0 = wall_clock64();
+    int in = W_G, o = W_S;
+    for (int i = 0; i < iters; i++) {
+      if (op == OP_SYNC) team_sync(t);
+      else if (op == OP_TEAM_CYC) team_op(t, o, [&](int c) { return w12_cyc_sqr_c(xld_w12(in), c); });
+      else team_op(t, o, [&](int c) { return w12_mul_c(xld_w12(in), xld_w12(W_G), c); });
+      const int x = in;
+      in = o;
+      o = x == W_G ? W_P : x;
+    }
+    t1 = wall_clock64();
+    keep = xld(in).x;
+  } else if (active) {
+    t0 = wall_clock64();
+#pragma unroll 1
+    for (int i = 0; i < iters; i++) {
+      switch (op) {
+        case OP_MULP: a = mulp(a, b); break;
+        case OP_DOT1: a = dot(a, b); break;
+        case OP_DOT3: a = dot(a, b, b, a, a, a); break;
+        case OP_DOT6: a = dot(a, b, b, a, a, a, b, b, a, b, b, a); break;
+        case OP_SQR2: a = sqr2(a); break;
+        case OP_INV2: a = inv_pair(a); break;
+        case OP_INV1: a = inv_pair(a, false); break;
+        default: a = is_zero2(a) ? b : add(a, zero()); break;
       }
     }
-    printf("}");
+    t1 = wall_clock64();
+    keep = a.x;
   }
-  printf("}}\n");
-  return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+  if (active && (threadIdx.x & 63u) == 0u) {
+    out[2 * w] = t1 - t0;
+    out[2 * w + 1] = keep;
+  }
+}
+
+int main() {
+  uint64_t* d;
+  if (hipMalloc(&d, 16 * sizeof(uint64_t)) != hipSuccess) return 1;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0) != hipSuccess || khz <= 0) return 1;
+  const double tick_us = 1000.0 / khz;
+  printf("{\"wall_clock_khz\": %d", khz);
+  for (int op = 0; op < OP_N; op++) {
+    for (int six = 0; six < (op < OP_SYNC ? 2 : 1); six++) {
+      const int iters = (op == OP_INV2 || op == OP_INV1) ? 20 : 400;
+      uint64_t h[16] = {};
+      for (int rep = 0; rep < 2; rep++) {  // the first launch warms the code object
+        hipMemset(d, 0, sizeof h);
+        hipLaunchKernelGGL(k_wvbench, dim3(1), dim3(512), 0, 0, op, six, iters, d);
+        if (hipDeviceSynchronize() != hipSuccess) return 2;
+      }
+      hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost);
+      uint64_t mx = 0;
+      for (int w = 0; w < 8; w++) mx = h[2 * w] > mx ? h[2 * w] : mx;
+      printf(", \"%s%s\": %.3f", NAMES[op], op < OP_SYNC ? (six ? "_six" : "_lone") : "", mx * tick_us / iters);
+    }
+  }
+  printf(", \"unit\": \"us per op\"}\n");
+  return 0;
 }

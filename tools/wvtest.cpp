@@ -128,7 +128,7 @@ static int cmd_verify() {
   return 0;
 }
 
-// tverify: as verify, by the four-wave team (wvteam.h), one host thread per wave
+// tverify: as verify, by the eight-wave team (wvteam.h), one host thread per wave
 static int cmd_tverify() {
   char a[300], b[4000], c[300];
   while (scanf("%299s %3999s %299s", a, b, c) == 3) {
@@ -146,9 +146,9 @@ static int cmd_tverify() {
     uint32_t b0[8];
     msg_b0(msg, b0);
     for (auto& ctr : g_host_ctr) ctr.store(0);
-    int cls[4];
-    std::thread th[4];
-    for (int w = 0; w < 4; w++)
+    int cls[TEAM_WAVES];
+    std::thread th[TEAM_WAVES];
+    for (int w = 0; w < TEAM_WAVES; w++)
       th[w] = std::thread([&, w]() {
         g_host_wave = w;
         wv_init();
@@ -157,7 +157,7 @@ static int cmd_tverify() {
         cls[w] = verify_team(sig.data(), b0, P.x.l, P.y.l, pinf, sx, sy, sinf);
       });
     for (auto& t : th) t.join();
-    for (int w = 1; w < 4; w++)
+    for (int w = 1; w < TEAM_WAVES; w++)
       if (cls[w] != cls[0]) fprintf(stderr, "waves disagree: %d vs %d\n", cls[w], cls[0]), abort();
     printf("%d\n", cls[0]);
     fflush(stdout);
