@@ -153,6 +153,7 @@ def main():
     pl = limbs25(P)
     for i in range(16):
         add(f"PC{i}", [pl[(l % 32) - i] if i <= (l % 32) <= i + 15 else 0 for l in range(64)])
+    add_dup("C1200_DUP", pow(2, 1200, P), montgomery=False)  # wave GCD's y^-1 (y = a 2^400) -> 400-form
     np25 = limbs25((-pow(P, -1, R)) % R)
     p_over_r = P / R
 

@@ -31,7 +31,7 @@
 #define BLS_HOST
 #endif
 #endif
-#include "fp.h"  // the batch engine's binary-GCD inversion, run here on wave-uniform values
+#include "fp.h"  // shared constants (exponents of the square root and the inverse)
 
 #ifdef WV_HOST
 #include <execinfo.h>
@@ -425,14 +425,10 @@ WVI F mul_xi(const F& a) {  // (1 + i) a = (a0 - a1) + (a0 + a1) i
 // carry-in mask of an exact carry chain over 16 limbs: generate g (limb == 2^25, or a borrow source),
 // propagate pm (limb == 2^25 - 1, or equal limbs); c_0 = 0, c_{k+1} = g_k | (pm_k & c_k). The
 // masks are wave-uniform (ballots), so this is scalar work.
-WVI uint32_t carry_in_mask(uint32_t g, uint32_t pm) {
-  uint32_t c = 0, cin = 0;
-  for (int k = 0; k < 16; k++) {
-    c |= cin << k;
-    cin = ((g >> k) & 1u) | (((pm >> k) & 1u) & cin);
-  }
-  return c;
-}
+// As one binary addition (g and pm are disjoint): with x = g | pm, y = g the carries of x + y are
+// generated where both bits are set (g) and propagated where exactly one is (pm), so the carry-in bits
+// are (x + y) ^ x ^ y = ((g | pm) + g) ^ pm -- three scalar operations instead of a 16-step chain.
+WVI uint32_t carry_in_mask(uint32_t g, uint32_t pm) { return (((g | pm) + g) ^ pm) & 0xFFFFu; }
 WVI V mask_to_lanes(uint32_t m_half0, uint32_t m_half1) {
   const V l = lane_id();
   const V bits = sel(l < 32u, vsplat(m_half0), vsplat(m_half1));
@@ -514,12 +510,9 @@ WVI F pow_pair(const F& a, const uint32_t (&e)[NW]) {
   }
   return r;
 }
-// ------------------------------------------------------------------ inversion by binary GCD
-// Both halves' canonical values are read out (v_readlane) as 12-word integers; fp.h's binary GCD
-// (Pornin, 25 x 31 divsteps on 64-bit approximations) runs on them as wave-uniform scalar code, its
-// exponentiation fallback included; the result goes back into the lanes. The GCD inverts the raw
-// integer a' = A 2^400 as if it were a 2^392-Montgomery value: it returns 2^784 / a', and one
-// product with the constant 2^416 turns that into 2^800 / a' = A^-1 2^400.
+WVI F inv_pair_pow(const F& a) { return pow_pair<12>(a, bls::EXP_P_MINUS_2); }  // 0 -> 0
+WVI F pow_pm3d4(const F& a) { return pow_pair<12>(a, bls::EXP_P_MINUS_3_DIV_4); }  // sqrt and its inverse
+// strict limbs of half h -> 12 little-endian 32-bit words (wave-uniform; wrecover.h's compression)
 WVI void limbs_to_words(V strict_limbs, int h, uint32_t (&w)[12]) {
   uint32_t limb[16];
   for (int k = 0; k < 16; k++) limb[k] = lane_val(strict_limbs, 32 * h + k);
@@ -531,55 +524,164 @@ WVI void limbs_to_words(V strict_limbs, int h, uint32_t (&w)[12]) {
     w[j] = (uint32_t)v;
   }
 }
-// 12-word integers (< 2^384) of half 0 and half 1 -> value-form limbs (not reduced mod p)
-WVI V words_to_limbs(const uint32_t (&w0)[12], const uint32_t (&w1)[12]) {
-  const V l = lane_id(), k = l & 15u;
-  V v = vsplat(0);
-  for (int kk = 0; kk < 16; kk++) {
-    const int bit = 25 * kk, wi = bit >> 5, sh = bit & 31;
-    auto pick = [&](const uint32_t (&w)[12]) {
-      const uint32_t lo = w[wi], hi = wi + 1 < 12 ? w[wi + 1] : 0u;
-      return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & M25;
-    };
-    v = sel(k == (uint32_t)kk, sel(l < 32u, vsplat(pick(w0)), vsplat(pick(w1))), v);
-  }
-  return sel((l & 16u) == 0u, v, vsplat(0));
+
+// ------------------------------------------------------------------ inversion by a lane-parallel GCD
+// The same binary GCD as fp.h fp_inv_bingcd_raw (Pornin: divsteps driven by 64-bit approximations of
+// a and b, the accumulated 2x2 matrix then applied to the full-width values), restated for the lanes
+// so that only the divsteps stay scalar: the four integers of the extended GCD -- a, b and their
+// cofactors u, v with a = u y, b = v y (mod p) -- are the four DPP rows of ONE register, 16 signed
+// limbs of 25 bits each. Each of the 31 iterations runs 25 divsteps on wave-uniform scalars, then
+//   all four rows  t = own * c_own + partner * c_partner   (v_mad_i64_i32; partner = the other row
+//                  of the pair via v_permlane16_swap; (a, b) and (u, v) take the same matrix)
+//   rows u, v      t += m p with m = t_0 (-p^-1) mod 2^25, so every row is divisible by 2^25
+//   all rows       one limb down (exact division by 2^25), three carry rounds
+//   rows a, b      exact carries (ballots), and a negative result negated together with its cofactor
+// 31 x 25 = 775 >= 761 divsteps; b ends at 1 and v = y^-1 (mod p), |v| < 32 p. The input y is the
+// canonical 400-form value A 2^400, so A^-1 2^400 = v 2^800 = mulp(v, 2^1200).
+constexpr int GCD_ITERS = 31, GCD_STEPS = 25;
+
+WVI V64 sel64(M c, V64 a, V64 b) { return join64(sel(c, lo32(a), lo32(b)), sel(c, hi32(a), hi32(b))); }
+template <int j>
+WVI V64 row_shl64(V64 x) {
+  return join64(row_shl<j>(lo32(x)), row_shl<j>(hi32(x)));
 }
-WVI void gcd_inverse_words(uint32_t (&w)[12]) {
+template <int j>
+WVI V64 row_shr64(V64 x) {
+  return join64(row_shr<j>(lo32(x)), row_shr<j>(hi32(x)));
+}
+// exact limbs of the rows in `rows` (bit r = DPP row r): lanes 0..14 from [-1, 2^25] to [0, 2^25),
+// the top lane (15) signed and unbounded -- one carry pass, then one borrow pass
+WVI V gcd_exact(V x, uint32_t rows) {
+  const V l = lane_id(), k = l & 15u, row = l >> 4;
+  const M low = (k != 15u) & (((vsplat(rows) >> row) & 1u) != 0u);
+  auto pass = [&](M gen, M prop) {
+    const uint64_t g = ballot(low & gen), pm = ballot(low & prop);
+    V in = vsplat(0);
+    for (int r = 0; r < 4; r++) {
+      if (!((rows >> r) & 1u)) continue;
+      const uint32_t c = carry_in_mask((uint32_t)(g >> (16 * r)) & 0xFFFFu, (uint32_t)(pm >> (16 * r)) & 0xFFFFu);
+      in = sel(row == (uint32_t)r, (vsplat(c) >> k) & 1u, in);
+    }
+    return in;
+  };
+  const V cin = pass(x == (1u << 25), x == M25);
+  x = x + cin;
+  x = sel(low & (x >= (1u << 25)) & (x < 0x80000000u), x - (1u << 25), x);  // 2^25, 2^25 + 1 (not -1)
+  const V bin = pass(x == 0xFFFFFFFFu, x == 0u);
+  x = x - bin;
+  return sel(low & (x >= 0x80000000u), x + (1u << 25), x);
+}
+// three carry rounds of signed 64-bit limbs (the top lane keeps its carries); limbs of |t| < 2^52 end
+// in [-1, 2^25] as 32-bit two's complement
+WVI V gcd_carry(V64 t) {
+  const M topl = (lane_id() & 15u) == 15u;
+  for (int r = 0; r < 3; r++) {
+    const V64 c = sar64(t, 25);
+    const V64 low = sel64(topl, t, join64(lo32(t) & M25, vsplat(0)));
+    t = add64(low, row_shr64<1>(sel64(topl, vsplat64(0), c)));
+  }
+  return lo32(t);
+}
+// [a0^-1 | a0^-1] (0 -> 0); returns false (and leaves r alone) if the divsteps did not reach b = 1
+WVI bool inv_gcd_lanes(const F& a, F& r) {
   WV_COUNT(OPC_GCD);
-  bls::u12 y;
-  for (int i = 0; i < 12; i++) y[i] = w[i];
-  bool conv;
-  bls::u12 r = bls::fp_inv_bingcd_raw(y, conv);
-  if (!conv) r = bls::fp_pow_p_minus_2(y);  // never taken on any input the fuzz has seen (fp.h)
-  for (int i = 0; i < 12; i++) w[i] = r[i];
-}
-// per half: a_h^-1 (0 -> 0); `both` = false when only half 0 is needed (a duplicated value)
-WVI F inv_pair(const F& a, bool both = true) {
+  const V l = lane_id(), k = l & 15u, row = l >> 4;
+  const M ev = (row & 1u) == 0u;
   const V c = canon_times(a, WC_ONE_DUP);
-  uint32_t w0[12], w1[12];
-  limbs_to_words(c, 0, w0);
-  gcd_inverse_words(w0);
-  if (both) {
-    limbs_to_words(c, 1, w1);
-    gcd_inverse_words(w1);
-  } else {
-    for (int i = 0; i < 12; i++) w1[i] = w0[i];
+  const V P = cword(WC_P_DUP), Pall = pl16_swap(P, P).a;  // p in every row
+  V x = sel(row == 0u, c, sel(row == 1u, Pall, sel((row == 2u) & (k == 0u), vsplat(1), vsplat(0))));
+  const uint32_t np0 = NP25[0];
+#pragma unroll 1
+  for (int it = 0; it < GCD_ITERS; it++) {
+    // 64-bit approximations of a (row 0) and b (row 1), fp.h's: low 31 bits, and the 33 bits below
+    // the top of the longer one
+    const uint64_t nzb = ballot((l < 32u) & (x != 0u));
+    const uint32_t nzr = ((uint32_t)nzb | (uint32_t)(nzb >> 16)) & 0xFFFFu;
+    const int top = msb16(nzr);
+    int n = 64;
+    if (top >= 0) {
+      const uint32_t tv = lane_val(x, top) | lane_val(x, 16 + top);
+      const int nb = 25 * top + 32 - __builtin_clz(tv);
+      n = nb > 64 ? nb : 64;
+    }
+    const int s = n - 33, i0 = s / 25, o = s % 25;
+    auto approx = [&](int base) -> uint64_t {
+      const uint64_t L0 = lane_val(x, base + i0), L1 = i0 + 1 < 16 ? lane_val(x, base + i0 + 1) : 0u,
+                     L2 = i0 + 2 < 16 ? lane_val(x, base + i0 + 2) : 0u;
+      const uint64_t hi = ((L0 >> o) | (L1 << (25 - o)) | (L2 << (50 - o))) & ((1ull << 33) - 1);
+      const uint64_t lo = ((uint64_t)lane_val(x, base) | ((uint64_t)lane_val(x, base + 1) << 25)) & 0x7fffffffull;
+      return lo | (hi << 31);
+    };
+    uint64_t A = approx(0), B = approx(16);
+    int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+    for (int j = 0; j < GCD_STEPS; j++) {
+      const bool odd = (A & 1u) != 0, sw = odd & (A < B);  // (32-bit halves compared on the scalar
+                                                             // unit measured 7% slower than this)
+      const uint64_t A2 = sw ? B : A, B2 = sw ? A : B;
+      const int32_t F0 = sw ? f1 : f0, G0 = sw ? g1 : g0, F1 = sw ? f0 : f1, G1 = sw ? g0 : g1;
+      A = odd ? A2 - B2 : A2;
+      f0 = odd ? F0 - F1 : F0;
+      g0 = odd ? G0 - G1 : G0;
+      B = B2;
+      f1 = F1 * 2;
+      g1 = G1 * 2;
+      A >>= 1;
+    }
+    // rows (a, u) take (f0, g0), rows (b, v) take (f1, g1), each against its pair partner
+    const VP swp = pl16_swap(x, x);
+    const V oth = sel(ev, swp.b, swp.a);
+    const V cown = sel(ev, vsplat((uint32_t)f0), vsplat((uint32_t)g1));
+    const V coth = sel(ev, vsplat((uint32_t)g0), vsplat((uint32_t)f1));
+    V64 t = smad(x, cown, smad(oth, coth, vsplat64(0)));
+    const uint32_t mu = (lane_val(lo32(t), 32) * np0) & M25, mv = (lane_val(lo32(t), 48) * np0) & M25;
+    t = add64(t, mad(sel(row == 2u, vsplat(mu), sel(row == 3u, vsplat(mv), vsplat(0))), Pall, vsplat64(0)));
+    // exact division by 2^25: limb 0 (a multiple of 2^25) carries into limb 1, then one limb down
+    const V64 q = sar64(t, 25);
+    t = add64(row_shl64<1>(t), sel64(k == 0u, q, vsplat64(0)));
+    x = gcd_exact(gcd_carry(t), 0x3u);
+    const bool na = (int32_t)lane_val(x, 15) < 0, nb = (int32_t)lane_val(x, 31) < 0;
+    if (na | nb) {
+      const V sa = vsplat(na ? 1u : 0u), sb = vsplat(nb ? 1u : 0u);
+      const M neg_ab = ((row == 0u) & (sa != 0u)) | ((row == 1u) & (sb != 0u));
+      const M neg_uv = ((row == 2u) & (sa != 0u)) | ((row == 3u) & (sb != 0u));
+      // -X = ones' complement + 1 on an exact row; a redundant cofactor row just negates its limbs
+      x = sel(neg_ab, sel(k != 15u, M25 - x, 0xFFFFFFFFu - x) + sel(k == 0u, vsplat(1), vsplat(0)), sel(neg_uv, 0u - x, x));
+      x = gcd_exact(x, 0x3u);
+    }
   }
-  // the GCD's output is < 2p: as a product operand it is a value below 2p
-  return mulp(mkF(words_to_limbs(w0, w1), 2.0), cst(WC_C416_DUP));
+  const uint64_t bnz = ballot((row == 1u) & (x != sel(k == 0u, vsplat(1), vsplat(0))));
+  const uint64_t ynz = ballot((row == 0u) & (c != 0u));
+  const bool y_zero = (ynz & 0xFFFFull) == 0;
+  if (bnz != 0 && !y_zero) return false;
+  // v (row 3) into both halves' even rows, + 32 p (non-negative), exact limbs
+  const V h1 = pl32_swap(x, x).b;
+  V v = sel(ev, pl16_swap(h1, h1).b, vsplat(0));
+  v = sel(ev, v + (P << 5), vsplat(0));
+  v = gcd_carry(join64(v, sel(sar32(v, 31) != 0u, vsplat(0xFFFFFFFFu), vsplat(0))));
+  v = gcd_exact(v, 0x5u);
+  if (y_zero) v = vsplat(0);
+  r = mulp(mkF(v, 64.0), cst(WC_C1200_DUP));
+  return true;
 }
+
+// [a0^-1 | a0^-1] (0 -> 0): the lane GCD, or the exponentiation if its divsteps did not reach b = 1
+// (no input of the host fuzz, tests/test_wv_host.py, takes that branch)
+WVI F inv_dup(const F& a) {
+  F r;
+  if (inv_gcd_lanes(a, r)) return r;
+  return inv_pair_pow(dup0(a));
+}
+
 // per half: a_h^-1 for two NONZERO halves, one GCD (Montgomery's trick): 1 / (a0 a1) times the
 // other half
 WVI F inv_pair_nz(const F& a) {
   const F other = swap_halves(a);
-  const F ni = inv_pair(mulp(a, other), false);
+  const F ni = inv_dup(mulp(a, other));
   return mulp(ni, other);
 }
-WVI F inv_pair_pow(const F& a) { return pow_pair<12>(a, bls::EXP_P_MINUS_2); }  // 0 -> 0
-WVI F pow_pm3d4(const F& a) { return pow_pair<12>(a, bls::EXP_P_MINUS_3_DIV_4); }  // sqrt and its inverse
+
 WVI F inv2(const F& a) {  // Fp2: conj(a) / N(a) (the norm is duplicated: one GCD)
-  const F ni = inv_pair(norm_dup(a), false);
+  const F ni = inv_dup(norm_dup(a));
   return mulp(conj<0>(a), ni);
 }
 

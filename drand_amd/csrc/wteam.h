@@ -5,8 +5,8 @@
 //
 //   exchange  a value lives in an LDS slot of 64 words (lane l's word at l); xst / xld
 //   team sync a monotonic LDS counter per team: every wave adds one and waits for gen * n -- waves of
-//             different teams run different code, so the workgroup barrier (which every wave must
-//             reach equally often) only separates phases
+//             different teams run different code; a team of the whole workgroup (phases B and C,
+//             where every wave runs the same sequence of syncs) uses the hardware barrier instead
 //
 // Host build: each wave of the workgroup is a std::thread running the same function (wvtest), the
 // slots carry their values' bounds, and the counters are std::atomic.
@@ -74,11 +74,17 @@ struct Team {
   int n, id;     // members; this wave's index among them (waves in increasing order)
   int ctr;       // its counter
   uint32_t gen;  // syncs passed
+  bool whole;    // every wave of the workgroup: team_sync is the hardware barrier
 };
 // the waves of `mask` (bit w = wave w); only members may call team_sync
 WVI Team make_team(uint32_t mask, int ctr) {
   const uint32_t below = mask & ((1u << wave_id()) - 1u);
-  return {__builtin_popcount(mask), __builtin_popcount(below), ctr, 0u};
+#ifdef WV_HOST
+  const bool whole = false;
+#else
+  const bool whole = __builtin_popcount(mask) * 64 == (int)blockDim.x;
+#endif
+  return {__builtin_popcount(mask), __builtin_popcount(below), ctr, 0u, whole};
 }
 
 WVI void team_sync(Team& t) {
@@ -88,6 +94,10 @@ WVI void team_sync(Team& t) {
   g_host_ctr[t.ctr].fetch_add(1, std::memory_order_acq_rel);
   while (g_host_ctr[t.ctr].load(std::memory_order_acquire) < target) std::this_thread::yield();
 #else
+  if (t.whole) {  // every wave takes the same sequence of whole-team syncs (uniform control flow)
+    __syncthreads();
+    return;
+  }
   uint32_t* c = blk_base() + BLK_SLOTS * 64 + BLK_WORDS_EXTRA + t.ctr;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (threadIdx.x % 64 == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

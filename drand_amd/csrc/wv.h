@@ -123,6 +123,23 @@ WVI V64 operator>>(const V64& a, int s) {
   WV_LANES r.v[l] = a.v[l] >> s;
   return r;
 }
+// acc + (int32)a * (int32)b, two's complement (v_mad_i64_i32)
+WVI V64 smad(const V& a, const V& b, const V64& acc) {
+  V64 r;
+  WV_LANES r.v[l] = acc.v[l] + (uint64_t)((int64_t)(int32_t)a.v[l] * (int64_t)(int32_t)b.v[l]);
+  return r;
+}
+// arithmetic shift of the two's-complement value
+WVI V64 sar64(const V64& a, int s) {
+  V64 r;
+  WV_LANES r.v[l] = (uint64_t)((int64_t)a.v[l] >> s);
+  return r;
+}
+WVI V sar32(const V& a, int s) {
+  V r;
+  WV_LANES r.v[l] = (uint32_t)((int32_t)a.v[l] >> s);
+  return r;
+}
 WVI V64 widen(const V& a) {
   V64 r;
   WV_LANES r.v[l] = a.v[l];
@@ -231,6 +248,9 @@ WVI V64 vsplat64(uint64_t s) { return s; }
 WVI V sel(M c, V a, V b) { return c ? a : b; }
 WVI V lane_id() { return __lane_id(); }
 WVI V64 mad(V a, V b, V64 acc) { return acc + (uint64_t)a * b; }
+WVI V64 smad(V a, V b, V64 acc) { return acc + (uint64_t)((int64_t)(int32_t)a * (int64_t)(int32_t)b); }
+WVI V64 sar64(V64 a, int s) { return (uint64_t)((int64_t)a >> s); }
+WVI V sar32(V a, int s) { return (uint32_t)((int32_t)a >> s); }
 WVI V64 widen(V a) { return a; }
 WVI V64 add64(V64 a, V64 b) { return a + b; }
 WVI V lo32(V64 a) { return (uint32_t)a; }

@@ -2,7 +2,8 @@
 // (k_lat.hip). The work of wverify.h's verify_item, scheduled across the waves:
 //
 //   phase A  wave 0: hash-to-G2 of the message at raised issue priority; waves 4, 5 join it for the
-//            cofactor clearing (team_clear_cofactor: each doubling in three rounds)
+//            cofactor clearing (team_clear_cofactor: each doubling in three rounds, each chain
+//            addition in five)
 //            wave 1: decompression of the signature, then its subgroup check
 //            waves 2, 3, 6, 7: as soon as wave 1 has the point, the Miller loop of the signature
 //            pair (e(-g1, S)) -- the subgroup check runs beside it, its verdict joins at the end
@@ -53,6 +54,11 @@ constexpr int CTR_ALL = 0, CTR_SIG = 1, CTR_DEC = 2, CTR_HASH = 3;
 // the hash team's slots during phase A: the key pair's area (free until phase B)
 constexpr int HS_P = TB0, HS_ACC = TB0 + 3, HS_A = TB0 + 6, HS_B = TB0 + 7, HS_C = TB0 + 8, HS_D = TB0 + 9,
               HS_EE = TB0 + 10, HS_Q2 = TB0 + 11;
+// the chain additions: the base's Z^2, Z^3, -2 Z^3, then the step's intermediates
+constexpr int HS_BZZ = TB0 + 14, HS_BZC = TB0 + 15, HS_BM2 = TB0 + 16, HS_ZZ = TB0 + 17, HS_U1 = TB0 + 18,
+              HS_Y2Z1 = TB0 + 19, HS_H = TB0 + 20, HS_R = TB0 + 21, HS_S1 = TB0 + 22, HS_I = TB0 + 23,
+              HS_Z2H = TB0 + 24, HS_RR = TB0 + 25, HS_J = TB0 + 26, HS_V = TB0 + 27;
+constexpr int XW_AINF = 16, XW_HZ = 17, XW_BINF = 18;
 
 WVI W12 xld_w12(int base, bool cj = false) {
   W12 r;
@@ -106,16 +112,76 @@ WVI void team_g2_dbl(Team& t, int acc) {
   }
   team_sync(t);
 }
-// acc <- [|x|] acc (wcurve.h g2_mul_x_abs, acc == base on entry): the doublings by the team, the five
-// additions (with their exceptional cases) on its first wave
+// acc <- acc + base (wcurve.h g2_add: add-2007-bl with its exceptional cases) in five rounds, the base's
+// Z^2, Z^3, -2 Z^3 and infinity flag prepared by team_mul_x_abs:
+//   Z1Z1, U1 = X1 Z2^2, Y2 Z1, [acc = O?] | H = X2 Z1Z1 - U1, r = 2 (Y2 Z1 Z1Z1 - Y1 Z2^3), S1 = Y1 Z2^3 |
+//   I = (2H)^2, 2 Z2 H, r^2, [H = 0?] | J = H I, V = U1 I, Z3 = Z1 (2 Z2 H) |
+//   X3 = r^2 - J - 2V, Y3 = r (3V + J - r^2) - 2 S1 J   (= r (V - X3) - 2 S1 J)
+WVI void team_g2_add_fixed(Team& t, int acc, int base) {
+  if (xld_word(XW_BINF)) return;  // acc + O
+  for (int j = t.id; j < 4; j += t.n) {
+    const F Z1 = xld(acc + 2);
+    if (j == 0) xst(HS_ZZ, sqr2(Z1));
+    else if (j == 1) xst(HS_U1, dot(xld(acc), xld(HS_BZZ)));
+    else if (j == 2) xst(HS_Y2Z1, dot(xld(base + 1), Z1));
+    else xst_word(XW_AINF, is_zero2(Z1) ? 1u : 0u);
+  }
+  team_sync(t);
+  if (xld_word(XW_AINF)) {  // O + base
+    if (t.id == 0) xst_g2(acc, xld_g2(base));
+    team_sync(t);
+    return;
+  }
+  for (int j = t.id; j < 3; j += t.n) {
+    const F Y1 = xld(acc + 1);
+    if (j == 0) xst(HS_H, dot(xld(base), xld(HS_ZZ), xld(HS_U1), cst(WC_NEG1)));
+    else if (j == 1) xst(HS_R, dot(xld(HS_Y2Z1), dbl(xld(HS_ZZ)), Y1, xld(HS_BM2)));
+    else xst(HS_S1, dot(Y1, xld(HS_BZC)));
+  }
+  team_sync(t);
+  for (int j = t.id; j < 4; j += t.n) {
+    const F H = xld(HS_H);
+    if (j == 0) xst(HS_I, dot(H, mul_small<4>(H)));
+    else if (j == 1) xst(HS_Z2H, dot(xld(base + 2), dbl(H)));
+    else if (j == 2) xst(HS_RR, sqr2(xld(HS_R)));
+    else xst_word(XW_HZ, is_zero2(H) ? 1u : 0u);
+  }
+  team_sync(t);
+  if (xld_word(XW_HZ)) {  // acc == +-base: doubling or the point at infinity
+    if (t.id == 0) xst_g2(acc, is_zero2(xld(HS_R)) ? g2_dbl(xld_g2(acc)) : g2_infinity());
+    team_sync(t);
+    return;
+  }
+  for (int j = t.id; j < 3; j += t.n) {
+    const F I = xld(HS_I);
+    if (j == 0) xst(HS_J, dot(xld(HS_H), I));
+    else if (j == 1) xst(HS_V, dot(xld(HS_U1), I));
+    else xst(acc + 2, dot(xld(acc + 2), xld(HS_Z2H)));
+  }
+  team_sync(t);
+  for (int j = t.id; j < 2; j += t.n) {
+    const F r = xld(HS_R), J = xld(HS_J), V = xld(HS_V);
+    if (j == 0) xst(acc, dot(r, r, J, cst(WC_NEG1), V, cst(WC_NEG2)));
+    else xst(acc + 1, dot(sub<0>(add(mul_small<3>(V), J), xld(HS_RR)), r, xld(HS_S1), neg<0>(dbl(J))));
+  }
+  team_sync(t);
+}
+// acc <- [|x|] acc (wcurve.h g2_mul_x_abs, acc == base on entry): the doublings and the five additions
+// by the team
 WVI void team_mul_x_abs(Team& t, int base, int acc) {
+  if (t.id == 0) {
+    const F Z2 = xld(base + 2);
+    const F zz = sqr2(Z2), zc = dot(Z2, zz);
+    xst(HS_BZZ, zz);
+    xst(HS_BZC, zc);
+    xst(HS_BM2, dot(zc, cst(WC_NEG2)));
+    xst_word(XW_BINF, is_zero2(Z2) ? 1u : 0u);
+  }
+  team_sync(t);
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
     team_g2_dbl(t, acc);
-    if ((bls::BLS_X_ABS >> i) & 1ull) {
-      if (t.id == 0) xst_g2(acc, g2_add(xld_g2(acc), xld_g2(base)));
-      team_sync(t);
-    }
+    if ((bls::BLS_X_ABS >> i) & 1ull) team_g2_add_fixed(t, acc, base);
   }
 }
 // wcurve.h g2_clear_cofactor by the hash team: p is the first wave's (the others pass anything);
@@ -205,7 +271,13 @@ WVI void team_miller_dbl(Team& t, const MPair& m, int tb, int& cur) {
   for (int j = 0; j < 11; j++)
     if ((jobs >> j) & 1u) dbl_job1(j, m, tb, fin);
   team_sync(t);
-  for (int j = t.id; j < 9; j += t.n) dbl_job2(j, tb, fout);
+  if (t.n == 8) {
+    // waves 0..5 the six f^2 l coefficients (three-term products), wave 6 X3 and Z3, wave 7 Y3
+    dbl_job2(t.id, tb, fout);
+    if (t.id == 6) dbl_job2(8, tb, fout);
+  } else {
+    for (int j = t.id; j < 9; j += t.n) dbl_job2(j, tb, fout);
+  }
   team_sync(t);
   cur ^= 1;
 }

@@ -1,6 +1,6 @@
 """Parity of the latency path at the sizes it serves.
 
-Every host call of 1..lat_max items (default 2,048) runs on the latency engine (k_lat.hip: one
+Every host call of 1..lat_max items (default 1,024) runs on the latency engine (k_lat.hip: one
 workgroup per item, limbs across lanes), a second implementation of the arithmetic beside the batch
 pipeline (one lane per item). This file puts full-size batches through the DEFAULT routing and checks
 them three ways: against the same call forced onto the batch pipeline (set_lat_max(0)), forced onto
@@ -8,8 +8,8 @@ the latency path, and against the C oracle's reject classes (oracle/c/bls_oracle
 reference KAT) at every injected position and its successor:
 
   * a continuous 2,049-round chained history (tests/golden/chain2049.bin, make_chain_fixture.py)
-    through host verify_chained at n = 1,000 (configs[0]), 2,048 (= lat_max) and 2,049 (= lat_max + 1,
-    the batch side of the cut-over), with every class of the mixed golden injected at the first, a
+    through host verify_chained at n = 1,000 (configs[0]), 1,024 (= lat_max), 1,025 (= lat_max + 1,
+    the batch side of the cut-over) and 2,048, with every class of the mixed golden injected at the first, a
     middle, the last item and a 64-item edge (client/verify.go:146-163, chain/beacon.go:87-108);
   * the same through blsv_verify_prevs (stored PreviousSig per row: the drand.db loader's call);
   * a device-generated SEGMENTED history through blsv_verify_chained_dev's latency branch with a
@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NONE = (1 << 64) - 1
 BIG = 1 << 20
-LAT_MAX = 2048
+LAT_MAX = 1024  # blsverify.cpp kLatMaxDefault (test_default_cutover)
 
 # classes of the mixed golden (tests/golden/golden.json "mixed"): name -> source index there; the
 # decode classes are copied as bytes, the others are made from the local signature
@@ -95,17 +95,23 @@ def _expected_chained(C, pk, seed, sigs, touched):
     return want
 
 
+def test_default_cutover(engine):
+    prev = engine.set_lat_max(0)
+    engine.set_lat_max(prev)
+    assert prev == LAT_MAX
+
+
 def test_chain_fixture_accepts(engine, golden, chain, C):
     ch = golden["chained"]
     pk, seed = bytes.fromhex(ch["pk"]), bytes.fromhex(ch["genesis_seed"])
     engine.set_public_key(pk)
-    for n in (1000, LAT_MAX, LAT_MAX + 1):
+    for n in (1000, LAT_MAX, LAT_MAX + 1, 2048):
         d, b, l = _routes(engine, lambda: engine.verify_chained(1, seed, chain[:n]), n)
         for r in (d, b, l):
             assert all(r.ok) and r.first_bad is None and not any(r.reject_class)
 
 
-@pytest.mark.parametrize("n", [1000, LAT_MAX, LAT_MAX + 1])
+@pytest.mark.parametrize("n", [1000, LAT_MAX, LAT_MAX + 1, 2048])
 @pytest.mark.parametrize("kind", list(MIXED) + list(LOCAL))
 def test_chained_every_class_at_size(engine, golden, chain, C, n, kind):
     ch = golden["chained"]
@@ -250,7 +256,7 @@ def test_verify_messages_2048(engine, golden, C):
     ch = golden["chained"]
     pk = bytes.fromhex(ch["pk"])
     sk32 = int(ch["sk"], 16).to_bytes(32, "big")
-    n = LAT_MAX
+    n = 2048
     msgs = [hashlib.sha256(b"lat-scale %d" % i).digest() for i in range(n)]
     sigs = engine.sign(sk32, msgs)
     pos = [0, 64, 1023, n - 1]

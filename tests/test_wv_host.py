@@ -53,6 +53,25 @@ def test_field_ops_match_integers(wvtest):
         assert eq == (a == b) and z == (a == (0, 0))
 
 
+def test_lane_gcd_inverse(wvtest):
+    """wfield.h inv_gcd_lanes (the lane-parallel binary GCD behind every latency-path inversion):
+    random values and the structured inputs of tools/opcount invfuzz (powers of two, p minus powers
+    of two, p / 2^k, values next to p, small values), each inverse against Python's, and every input
+    must converge (no exponentiation fallback)."""
+    rng = random.Random(25)
+    vals = [0, 1, 2, 3, P - 1, P - 2, (P + 1) // 2, (P - 1) // 2]
+    vals += [1 << k for k in range(0, 381, 7)] + [P - (1 << k) for k in range(0, 380, 9)]
+    vals += [P >> k for k in range(1, 380, 11)] + [rng.randrange(1, 1 << 32) for _ in range(10)]
+    vals += [rng.randrange(P) for _ in range(400)]
+    vals = [v % P for v in vals]
+    out = run(wvtest, "inv", ["%x" % v for v in vals])
+    assert len(out) == len(vals)
+    for v, line in zip(vals, out):
+        assert line != "nc", hex(v)
+        want = pow(v, P - 2, P)
+        assert [int(x, 16) for x in line.split()] == [want, want], hex(v)
+
+
 def test_hash_to_g2_golden(wvtest, golden):
     cases = golden["hash_to_g2"]
     out = run(wvtest, "hash", [h["msg"] or "-" for h in cases])

@@ -16,7 +16,7 @@ using namespace wv;
 
 enum { OP_MULP, OP_DOT1, OP_DOT3, OP_DOT6, OP_SQR2, OP_INV2, OP_INV1, OP_ISZERO, OP_SYNC, OP_TEAM_CYC, OP_TEAM_MUL,
        OP_N };
-static const char* NAMES[OP_N] = {"mulp", "dot1", "dot3", "dot6", "sqr2", "inv_pair2", "inv_pair1", "is_zero2",
+static const char* NAMES[OP_N] = {"mulp", "dot1", "dot3", "dot6", "sqr2", "inv_pair_nz", "inv_dup", "is_zero2",
                                   "team_sync8", "team_cyc_sqr8", "team_mul8"};
 
 __global__ void __launch_bounds__(512) k_wvbench(int op, int six, int iters, uint64_t* out) {
@@ -60,8 +60,8 @@ __global__ void __launch_bounds__(512) k_wvbench(int op, int six, int iters, uin
         case OP_DOT3: a = dot(a, b, b, a, a, a); break;
         case OP_DOT6: a = dot(a, b, b, a, a, a, b, b, a, b, b, a); break;
         case OP_SQR2: a = sqr2(a); break;
-        case OP_INV2: a = inv_pair(a); break;
-        case OP_INV1: a = inv_pair(a, false); break;
+        case OP_INV2: a = inv_pair_nz(a); break;
+        case OP_INV1: a = inv_dup(a); break;
         default: a = is_zero2(a) ? b : add(a, zero()); break;
       }
     }

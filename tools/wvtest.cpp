@@ -3,6 +3,7 @@
 // Python integers and the golden vectors on the CPU.
 //
 // usage: wvtest field   < lines "a0 a1 b0 b1" (hex, raw values < p)  -> one line of results each
+//        wvtest inv     < lines "a" (hex, raw < p)                    -> raw a^-1 in both halves (lane GCD)
 //        wvtest verify  < lines "pk48 msg sig96" (hex)                -> reject class per line
 //        wvtest hash    < lines "msg" (hex)                            -> affine H(msg) raw hex
 //        wvtest pair    < lines "px py qx0 qx1 qy0 qy1" (affine raw)  -> Miller loop + final exp (raw)
@@ -86,6 +87,24 @@ static int cmd_field() {
     printf(" %s", out_fp2(dot(a, b, b, a, a, a)).c_str());
     printf(" %d %d", (int)eq2(a, b), (int)is_zero2(a));
     printf("\n");
+  }
+  return 0;
+}
+
+// inv: "a" (hex, raw < p) -> raw a^-1 (0 -> 0) by the lane GCD, or "nc" if its divsteps did not
+// reach b = 1 (the caller would take the exponentiation)
+static int cmd_inv() {
+  char a0[200];
+  while (scanf("%199s", a0) == 1) {
+    wv_init();
+    const F a = to_mont(raw_fp2(a0, a0));
+    F r;
+    if (!inv_gcd_lanes(a, r)) {
+      printf("nc\n");
+      continue;
+    }
+    const V c = raw_canon(r);
+    printf("%s %s\n", limbs_to_hex(c, 0).c_str(), limbs_to_hex(c, 1).c_str());
   }
   return 0;
 }
@@ -272,6 +291,7 @@ static int cmd_smul() {
 
 int main(int argc, char** argv) {
   if (argc >= 2 && !strcmp(argv[1], "field")) return cmd_field();
+  if (argc >= 2 && !strcmp(argv[1], "inv")) return cmd_inv();
   if (argc >= 2 && !strcmp(argv[1], "verify")) return cmd_verify();
   if (argc >= 2 && !strcmp(argv[1], "tverify")) return cmd_tverify();
   if (argc >= 2 && !strcmp(argv[1], "hash")) return cmd_hash();
