@@ -485,7 +485,9 @@ WVI uint32_t lane0_of_half(V x, int h) { return lane_val(x, 32 * h); }
 
 // ------------------------------------------------------------------ exponentiation (pair)
 // a^e per half, e = public exponent as NW little-endian 32-bit words (wave-uniform): 4-bit fixed
-// window, table a^0..a^15 in registers, digits from the top
+// window, table a^0..a^15 in registers, digits from the top. (A 5-bit sliding window over odd powers
+// does 457 products for (p-3)/4 against 481 here but measured 7% slower: r04u, its runtime windows
+// and table index)
 template <int NW>
 WVI F pow_pair(const F& a, const uint32_t (&e)[NW]) {
   F t[16];

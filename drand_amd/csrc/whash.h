@@ -106,8 +106,15 @@ WVI bool sgn0_fp2(const F& a) {
   return s0 | (z0 & s1);
 }
 
-// both SSWU maps of a hash: (x_m, y_m) on E2' for u_m (hash.h map_to_curve_sswu with its tv1)
-WVI void sswu2(const F (&u)[2], F (&xo)[2], F (&yo)[2]) {
+// a^((p-3)/4) on this wave alone (the team form hands the squarings' powers to a helper wave)
+struct PowSelf {
+  WVI F operator()(const F& a) const { return pow_pm3d4(a); }
+};
+
+// both SSWU maps of a hash: (x_m, y_m) on E2' for u_m (hash.h map_to_curve_sswu with its tv1); pw
+// computes a^((p-3)/4) per half
+template <class Pow = PowSelf>
+WVI void sswu2(const F (&u)[2], F (&xo)[2], F (&yo)[2], Pow pw = Pow()) {
   const F Z = cst(WC_SSWU_Z), A = cst(WC_SSWU_A), B = cst(WC_SSWU_B);
   F zu2[2], den[2];
   uint32_t dz = 0;
@@ -129,7 +136,7 @@ WVI void sswu2(const F (&u)[2], F (&xo)[2], F (&yo)[2]) {
   }
   // root of the norms: w = n^((p-3)/4), r1 = w n; sq1 = r1^2 == n (N(gx1) a square)
   const F n = select_halves(1u, norm_dup(gx1[0]), norm_dup(gx1[1]));
-  const F r1 = mulp(pow_pm3d4(n), n);
+  const F r1 = mulp(pw(n), n);
   const uint32_t sq1 = zero_halves(sub<0>(sqrp(r1), n));
   // r2 = N(u)^3 sqrt(-N(Z)^3) r1 (the root for gx2 = (Z u^2)^3 gx1 when N(gx1) is not a square)
   const F nu = select_halves(1u, norm_dup(u[0]), norm_dup(u[1]));
@@ -148,7 +155,7 @@ WVI void sswu2(const F (&u)[2], F (&xo)[2], F (&yo)[2]) {
   F ap = half(add(a0, s));
   const F am = half(sub<0>(a0, s));
   ap = select_halves(zero_halves(ap), am, ap);
-  const F w = pow_pm3d4(ap);
+  const F w = pw(ap);
   const F t = mulp(w, ap);
   const uint32_t direct = zero_halves(sub<1>(sqrp(t), ap));
   const F inv2t = half(select_halves(direct, w, neg<0>(w)));
@@ -181,13 +188,14 @@ WVI G2J iso_map(const F& x, const F& y) {
 }
 
 // the sum of the two mapped points (before the cofactor clearing) from the message's xmd b_0
-WVI G2J hash_to_curve_sum(const uint32_t (&b0)[8]) {
+template <class Pow = PowSelf>
+WVI G2J hash_to_curve_sum(const uint32_t (&b0)[8], Pow pw = Pow()) {
   uint32_t e[4][16];
   xmd_words(b0, e);
   const F u[2] = {fp2_from_be512(e[0], e[1]), fp2_from_be512(e[2], e[3])};
   F x[2], y[2];
   WV_MARK(10);
-  sswu2(u, x, y);
+  sswu2(u, x, y, pw);
   WV_MARK(11);
   const G2J q = g2_add(iso_map(x[0], y[0]), iso_map(x[1], y[1]));
   WV_MARK(12);
@@ -207,7 +215,8 @@ WVI bool hash_to_g2(const uint32_t (&b0)[8], F& hx, F& hy) {
 // 96-byte compressed point (wave-uniform bytes) -> affine (x, y), kilic FromCompressed check order;
 // with subgroup = false the final subgroup check is left to the caller (wvteam.h runs it beside the
 // signature's Miller loop)
-WVI uint8_t g2_decompress(const uint8_t* in, F& ox, F& oy, bool& is_inf, bool subgroup = true) {
+template <class Pow = PowSelf>
+WVI uint8_t g2_decompress(const uint8_t* in, F& ox, F& oy, bool& is_inf, bool subgroup = true, Pow pw = Pow()) {
   is_inf = false;
   const uint8_t b0 = in[0];
   if (!(b0 & 0x80)) return bls::REJ_FLAG;
@@ -248,12 +257,12 @@ WVI uint8_t g2_decompress(const uint8_t* in, F& ox, F& oy, bool& is_inf, bool su
   const F rhs = dot(sqr2(x), x, cst(WC_B2), cst(WC_ONE2));  // x^3 + b'
   // sqrt through the norm: s = n^((p+1)/4) = w n, n a square iff s^2 == n
   const F n = norm_dup(rhs);
-  const F s = mulp(pow_pm3d4(n), n);
+  const F s = mulp(pw(n), n);
   bool ok = zero_halves(sub<0>(sqrp(s), n)) == 3u;
   // candidates [(a0 + s)/2 | (a0 - s)/2], both exponentiated at once; the second when the first is 0
   const F a0 = dup0(rhs);
   const F cand = half(select_halves(1u, add(a0, s), sub<0>(a0, s)));
-  const F wc = pow_pm3d4(cand);
+  const F wc = pw(cand);
   const int pick = (zero_halves(cand) & 1u) ? 1 : 0;
   const F ap = pick ? dup1(cand) : dup0(cand);
   const F w = pick ? dup1(wc) : dup0(wc);

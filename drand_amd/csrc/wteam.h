@@ -24,7 +24,7 @@ namespace wv {
 #define WV_BLK_SLOTS 128
 #endif
 constexpr int BLK_SLOTS = WV_BLK_SLOTS;
-constexpr int BLK_CTRS = 8;   // team counters
+constexpr int BLK_CTRS = 12;  // team counters
 constexpr int BLK_WORDS_EXTRA = 64;  // scalar words (verdicts, flags)
 
 #ifdef WV_HOST
@@ -116,6 +116,17 @@ WVI void flag_post(int ctr) {
 #else
   uint32_t* c = blk_base() + BLK_SLOTS * 64 + BLK_WORDS_EXTRA + ctr;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (threadIdx.x % 64 == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+}
+// flag_post for data this wave wrote to LDS only: a wave's ds operations execute in order in the LDS,
+// so a consumer that reads the counter's new value reads the data too; no wait for the stores
+WVI void flag_post_lds(int ctr) {
+#ifdef WV_HOST
+  g_host_ctr[ctr].fetch_add(1, std::memory_order_acq_rel);
+#else
+  uint32_t* c = blk_base() + BLK_SLOTS * 64 + BLK_WORDS_EXTRA + ctr;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // keeps the compiler from sinking the stores
   if (threadIdx.x % 64 == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
 }

@@ -1,10 +1,11 @@
 // One verification by a team of eight waves (two per SIMD of a CU), the latency engine's device form
 // (k_lat.hip). The work of wverify.h's verify_item, scheduled across the waves:
 //
-//   phase A  wave 0: hash-to-G2 of the message at raised issue priority; waves 4, 5 join it for the
-//            cofactor clearing (team_clear_cofactor: each doubling in three rounds, each chain
+//   phase A  wave 0: hash-to-G2 of the message at raised issue priority, wave 5 multiplying for its two
+//            SSWU exponentiations (ring_pow_*); waves 4, 5 join it for the cofactor clearing (team_clear_cofactor: each doubling in three rounds, each chain
 //            addition in five)
-//            wave 1: decompression of the signature, then its subgroup check
+//            wave 1: decompression of the signature (wave 2 multiplying for its square roots), then
+//            its subgroup check
 //            waves 2, 3, 6, 7: as soon as wave 1 has the point, the Miller loop of the signature
 //            pair (e(-g1, S)) -- the subgroup check runs beside it, its verdict joins at the end
 //   phase B  all eight: the Miller loop of the key pair (e(pk, H(m)))
@@ -78,6 +79,16 @@ WVI void team_op(Team& t, int dst, Fn fn) {
   for (int k = t.id; k < 6; k += t.n) xst(dst + k, fn(k));
   team_sync(t);
 }
+// the cyclotomic square's outputs by cost on the whole team: the three 2-term outputs (1, 3, 5) and
+// one 3-term output on the two SIMDs that carry two active waves (waves 0 and 4, 1 and 5), the other
+// two 3-term outputs alone on SIMDs 2 and 3
+template <class Fn>
+WVI void team_op_cyc(Team& t, int dst, Fn fn) {
+  if (t.n != 8) return team_op(t, dst, fn);
+  constexpr int8_t K[8] = {1, 5, 2, 4, 3, 0, -1, -1};
+  if (K[t.id] >= 0) xst(dst + K[t.id], fn(K[t.id]));
+  team_sync(t);
+}
 
 WVI void xst_g2(int base, const G2J& p) {
   xst(base, p.x);
@@ -85,6 +96,101 @@ WVI void xst_g2(int base, const G2J& p) {
   xst(base + 2, p.z);
 }
 WVI G2J xld_g2(int base) { return {xld(base), xld(base + 1), xld(base + 2)}; }
+
+// ------------------------------------------------------------------ exponentiation by two waves
+// a^e right to left: the producer squares (a, a^2, a^4, .. : the chain of 378 squarings) and hands
+// every power whose exponent bit is set to the consumer through a ring of LDS slots; the consumer
+// multiplies them up and hands the product back. The critical path is the squaring chain alone (the
+// fixed-window exponentiation's 91 products and 14-entry table leave it), the consumer's ~190
+// products run beside it on another SIMD. Two rings: the hash wave's (consumer wave 5) in the key
+// pair's area, the signature decoder's (consumer wave 2) in the signature pair's area (both free
+// until their Miller loops).
+constexpr int RING = 8;
+struct Ring {
+  int slot0, ctr0;  // RING slots + the result slot; counters produced, consumed, results
+};
+constexpr Ring HASH_RING = {TB0, 4}, SIG_RING = {TB1, 8};
+template <int NW>
+WVI int exp_bits(const uint32_t (&e)[NW]) {
+  int n = 0;
+  for (int i = 0; i < NW; i++) n = e[i] ? 32 * i + 32 - __builtin_clz(e[i]) : n;
+  return n;
+}
+template <int NW>
+WVI uint32_t exp_ones(const uint32_t (&e)[NW]) {
+  uint32_t c = 0;
+  for (int i = 0; i < NW; i++) c += (uint32_t)__builtin_popcount(e[i]);
+  return c;
+}
+struct RingCounts {
+  uint32_t produced = 0, consumed = 0, results = 0;
+};
+template <int NW>
+WVI F ring_pow_produce(const Ring& rg, const F& a, const uint32_t (&e)[NW], RingCounts& rc) {
+  const int nb = exp_bits(e);
+  F x = a;
+#pragma unroll 1
+  for (int i = 0; i < nb; i++) {
+    if ((e[i >> 5] >> (i & 31)) & 1u) {
+      if (rc.produced >= (uint32_t)RING) flag_wait(rg.ctr0 + 1, rc.produced - RING + 1);  // slot consumed
+      xst(rg.slot0 + rc.produced % RING, x);
+      flag_post_lds(rg.ctr0);
+      rc.produced++;
+    }
+    if (i + 1 < nb) x = sqrp(x);
+  }
+  rc.results++;
+  flag_wait(rg.ctr0 + 2, rc.results);
+  return xld(rg.slot0 + RING);
+}
+// one exponentiation's products; with stop_ctr >= 0, returns false without consuming when that counter
+// is posted before the first power arrives (the producer finished without this exponentiation)
+template <int NW>
+WVI bool ring_pow_consume(const Ring& rg, const uint32_t (&e)[NW], RingCounts& rc, int stop_ctr = -1) {
+  if (stop_ctr >= 0) {
+    uint32_t* c = blk_base() + BLK_SLOTS * 64 + BLK_WORDS_EXTRA;
+    for (;;) {
+#ifdef WV_HOST
+      const uint32_t prod = g_host_ctr[rg.ctr0].load(std::memory_order_acquire);
+      const uint32_t stop = g_host_ctr[stop_ctr].load(std::memory_order_acquire);
+#else
+      const uint32_t stop = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(c + stop_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      const uint32_t prod = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(c + rg.ctr0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+#endif
+      if (prod > rc.consumed) break;
+      if (stop) return false;
+#ifdef WV_HOST
+      std::this_thread::yield();
+#else
+      __builtin_amdgcn_s_sleep(1);
+#endif
+    }
+    (void)c;
+  }
+  const uint32_t ones = exp_ones(e);
+  F acc;
+#pragma unroll 1
+  for (uint32_t k = 0; k < ones; k++) {
+    flag_wait(rg.ctr0, rc.consumed + 1);
+    const F v = xld(rg.slot0 + rc.consumed % RING);
+    acc = k == 0 ? v : mulp(acc, v);
+    rc.consumed++;
+    flag_post(rg.ctr0 + 1);  // after the slot's read has returned (the producer reuses the slot)
+  }
+  xst(rg.slot0 + RING, acc);
+  flag_post(rg.ctr0 + 2);
+  return true;
+}
+// a^((p-3)/4) with a helper wave as the consumer
+struct PowRing {
+  const Ring* rg;
+  RingCounts* rc;
+  WVI F operator()(const F& a) const { return ring_pow_produce(*rg, a, bls::EXP_P_MINUS_3_DIV_4, *rc); }
+};
+constexpr int SSWU_POWS = 2;  // whash.h sswu2: the norms' root, then the candidates' root
+constexpr int DEC_POWS = 2;   // whash.h g2_decompress (none when it rejects before its square root)
 
 // ------------------------------------------------------------------ cofactor clearing by a team
 // wcurve.h g2_dbl (dbl-2009-l) in three rounds of one product per wave, on the accumulator's slots:
@@ -184,8 +290,72 @@ WVI void team_mul_x_abs(Team& t, int base, int acc) {
     if ((bls::BLS_X_ABS >> i) & 1ull) team_g2_add_fixed(t, acc, base);
   }
 }
+// acc <- acc + base for any two points (wcurve.h g2_add) in five rounds, the base's Z powers included:
+//   Z1^2, Z2^2, Y2 Z1, Y1 Z2, [acc = O?], [base = O?] | H = X2 Z1^2 - X1 Z2^2, r = 2 (Y2 Z1 Z1^2 - Y1 Z2 Z2^2),
+//   U1 = X1 Z2^2, S1 = Y1 Z2 Z2^2 | I = (2H)^2, 2 Z1 H, r^2, [H = 0?] | J = H I, V = U1 I, Z3 = (2 Z1 H) Z2 |
+//   X3, Y3 as team_g2_add_fixed
+WVI void team_g2_add(Team& t, int acc, int base) {
+  constexpr int S_Z2Z2 = HS_BZZ, S_Y1Z2 = HS_BZC;
+  for (int j = t.id; j < 6; j += t.n) {
+    const F Z1 = xld(acc + 2), Z2 = xld(base + 2);
+    if (j == 0) xst(HS_ZZ, sqr2(Z1));
+    else if (j == 1) xst(S_Z2Z2, sqr2(Z2));
+    else if (j == 2) xst(HS_Y2Z1, dot(xld(base + 1), Z1));
+    else if (j == 3) xst(S_Y1Z2, dot(xld(acc + 1), Z2));
+    else if (j == 4) xst_word(XW_AINF, is_zero2(Z1) ? 1u : 0u);
+    else xst_word(XW_BINF, is_zero2(Z2) ? 1u : 0u);
+  }
+  team_sync(t);
+  if (xld_word(XW_BINF)) return;  // acc + O
+  if (xld_word(XW_AINF)) {        // O + base
+    if (t.id == 0) xst_g2(acc, xld_g2(base));
+    team_sync(t);
+    return;
+  }
+  for (int j = t.id; j < 4; j += t.n) {
+    const F Z2Z2 = xld(S_Z2Z2);
+    if (j == 0) xst(HS_H, dot(xld(base), xld(HS_ZZ), xld(acc), neg<0>(Z2Z2)));
+    else if (j == 1) xst(HS_R, dot(xld(HS_Y2Z1), dbl(xld(HS_ZZ)), xld(S_Y1Z2), neg<0>(dbl(Z2Z2))));
+    else if (j == 2) xst(HS_U1, dot(xld(acc), Z2Z2));
+    else xst(HS_S1, dot(xld(S_Y1Z2), Z2Z2));
+  }
+  team_sync(t);
+  for (int j = t.id; j < 4; j += t.n) {
+    const F H = xld(HS_H);
+    if (j == 0) xst(HS_I, dot(H, mul_small<4>(H)));
+    else if (j == 1) xst(HS_Z2H, dot(xld(acc + 2), dbl(H)));
+    else if (j == 2) xst(HS_RR, sqr2(xld(HS_R)));
+    else xst_word(XW_HZ, is_zero2(H) ? 1u : 0u);
+  }
+  team_sync(t);
+  if (xld_word(XW_HZ)) {
+    if (t.id == 0) xst_g2(acc, is_zero2(xld(HS_R)) ? g2_dbl(xld_g2(acc)) : g2_infinity());
+    team_sync(t);
+    return;
+  }
+  for (int j = t.id; j < 3; j += t.n) {
+    const F I = xld(HS_I);
+    if (j == 0) xst(HS_J, dot(xld(HS_H), I));
+    else if (j == 1) xst(HS_V, dot(xld(HS_U1), I));
+    else xst(acc + 2, dot(xld(HS_Z2H), xld(base + 2)));
+  }
+  team_sync(t);
+  for (int j = t.id; j < 2; j += t.n) {
+    const F r = xld(HS_R), J = xld(HS_J), V = xld(HS_V);
+    if (j == 0) xst(acc, dot(r, r, J, cst(WC_NEG1), V, cst(WC_NEG2)));
+    else xst(acc + 1, dot(sub<0>(add(mul_small<3>(V), J), xld(HS_RR)), r, xld(HS_S1), neg<0>(dbl(J))));
+  }
+  team_sync(t);
+}
+// y <- -y of the point in slots p (one wave writes; the caller's next team round reads)
+WVI void team_neg_y(Team& t, int p) {
+  if (t.id == 0) xst(p + 1, neg<0>(xld(p + 1)));
+  team_sync(t);
+}
+
 // wcurve.h g2_clear_cofactor by the hash team: p is the first wave's (the others pass anything);
-// the result is the first wave's
+// the result is the first wave's. A = -[|x|] P + psi(P), then -[|x|] A - A - P + psi^2(2P), every
+// addition and doubling by the team
 WVI G2J team_clear_cofactor(Team& t, const G2J& p) {
   if (t.id == 0) {
     xst_g2(HS_P, p);
@@ -193,17 +363,31 @@ WVI G2J team_clear_cofactor(Team& t, const G2J& p) {
   }
   team_sync(t);
   team_mul_x_abs(t, HS_P, HS_ACC);
-  if (t.id == 0) {
-    const G2J a = g2_add(g2_neg(xld_g2(HS_ACC)), g2_psi(p));
-    xst_g2(HS_Q2, a);
-    xst_g2(HS_ACC, a);
+  // psi(P) into HS_Q2 (conj(x) kx, conj(y) ky, conj(z))
+  for (int j = t.id; j < 3; j += t.n) {
+    const F c = xld(HS_P + j);
+    xst(HS_Q2 + j, j == 2 ? conj<1>(c) : mul2(conj<1>(c), cst(j == 0 ? WC_PSI_KX : WC_PSI_KY)));
   }
   team_sync(t);
+  team_neg_y(t, HS_ACC);
+  team_g2_add(t, HS_ACC, HS_Q2);  // A
+  if (t.id == 0) xst_g2(HS_Q2, xld_g2(HS_ACC));
+  team_sync(t);
   team_mul_x_abs(t, HS_Q2, HS_ACC);
-  if (t.id != 0) return p;
-  G2J r = g2_add(g2_neg(xld_g2(HS_ACC)), g2_neg(xld_g2(HS_Q2)));
-  r = g2_add(r, g2_neg(p));
-  return g2_add(r, g2_psi2(g2_dbl(p)));
+  // -[|x|] A - A - P + psi^2(2P): HS_Q2 <- -A, then -P, then psi^2(2P) as the bases
+  if (t.id == 0) xst(HS_ACC + 1, neg<0>(xld(HS_ACC + 1)));
+  team_neg_y(t, HS_Q2);
+  team_g2_add(t, HS_ACC, HS_Q2);
+  if (t.id == 0) xst_g2(HS_Q2, g2_neg(xld_g2(HS_P)));
+  team_sync(t);
+  team_g2_add(t, HS_ACC, HS_Q2);
+  if (t.id == 0) xst_g2(HS_Q2, xld_g2(HS_P));
+  team_sync(t);
+  team_g2_dbl(t, HS_Q2);
+  for (int j = t.id; j < 2; j += t.n) xst(HS_Q2 + j, mulp(xld(HS_Q2 + j), cst(j == 0 ? WC_PSI2_KX : WC_PSI2_KY)));
+  team_sync(t);
+  team_g2_add(t, HS_ACC, HS_Q2);
+  return t.id == 0 ? xld_g2(HS_ACC) : p;
 }
 
 // ------------------------------------------------------------------ Miller loop of one pair
@@ -365,7 +549,7 @@ WVI void team_pow_x_abs(Team& t, int dst, int src, int scr) {
     const int n = (int)((NSQ >> (6 * s)) & 63u);
 #pragma unroll 1
     for (int k = 0; k < n; k++) {
-      team_op(t, out, [&](int c) { return w12_cyc_sqr_c(xld_w12(in), c); });
+      team_op_cyc(t, out, [&](int c) { return w12_cyc_sqr_c(xld_w12(in), c); });
       in = out;
       out = out == scr ? dst : scr;
     }
@@ -377,10 +561,56 @@ WVI void team_pow_x_abs(Team& t, int dst, int src, int scr) {
   }
 }
 
+// W_INV <- conj(f^-1) for the Fp12 value in slots f (wtower.h w12_inv<true>) in six rounds around one
+// inversion: f = A + B w, A = (c0, c2, c4), B = (c1, c3, c5), D = A^2 - v B^2 (each coefficient one
+// 4-term product straight from A and B) | t0 = D0^2 - xi D1 D2, t1 = xi D2^2 - D0 D1, t2 = D1^2 - D0 D2 |
+// d = D0 t0 + xi (D2 t1 + D1 t2) | 1/d (one wave) | D^-1 = t / d | (A D^-1, B D^-1)
+WVI void team_w12_inv_conj(Team& t, int f) {
+  constexpr int SD = W_T, ST = W_T + 3, SDI = W_U, SI = W_U + 1;  // D, t, 1/d, D^-1 (free slots)
+  for (int j = t.id; j < 3; j += t.n) {
+    const F a0 = xld(f), a1 = xld(f + 2), a2 = xld(f + 4), b0 = xld(f + 1), b1 = xld(f + 3), b2 = xld(f + 5);
+    F d;
+    if (j == 0)  // a0^2 + 2 xi a1 a2 - xi (2 b0 b2 + b1^2)
+      d = dot(a0, a0, a1, dbl(mul_xi<0>(a2)), b0, neg<1>(dbl(mul_xi<0>(b2))), b1, neg<1>(mul_xi<0>(b1)));
+    else if (j == 1)  // 2 a0 a1 + xi a2^2 - (b0^2 + 2 xi b1 b2)
+      d = dot(a0, dbl(a1), a2, mul_xi<0>(a2), b0, neg<0>(b0), b1, neg<1>(dbl(mul_xi<0>(b2))));
+    else  // 2 a0 a2 + a1^2 - (2 b0 b1 + xi b2^2)
+      d = dot(a0, dbl(a2), a1, a1, b0, neg<0>(dbl(b1)), b2, neg<1>(mul_xi<0>(b2)));
+    xst(SD + j, d);
+  }
+  team_sync(t);
+  for (int j = t.id; j < 3; j += t.n) {
+    const F c0 = xld(SD), c1 = xld(SD + 1), c2 = xld(SD + 2);
+    if (j == 0) xst(ST, dot(c0, c0, c2, neg<1>(mul_xi<0>(c1))));
+    else if (j == 1) xst(ST + 1, dot(c2, mul_xi<0>(c2), c1, neg<0>(c0)));
+    else xst(ST + 2, dot(c1, c1, c2, neg<0>(c0)));
+  }
+  team_sync(t);
+  if (t.id == 0) {
+    const F c0 = xld(SD), c1 = xld(SD + 1), c2 = xld(SD + 2);
+    const F d = dot(c0, xld(ST), mul_xi<0>(c2), xld(ST + 1), mul_xi<0>(c1), xld(ST + 2));
+    xst(SDI, inv2(d));
+  }
+  team_sync(t);
+  for (int j = t.id; j < 3; j += t.n) xst(SI + j, mul2(xld(ST + j), xld(SDI)));
+  team_sync(t);
+  for (int j = t.id; j < 6; j += t.n) {
+    // output slot k = 2 i + h: component i of (A or B) * D^-1 (h = 0: A, 1: B); conj keeps B's sign
+    const int h = j & 1, i = j >> 1;
+    const F x0 = xld(f + h), x1 = xld(f + 2 + h), x2 = xld(f + 4 + h);
+    const F y0 = xld(SI), y1 = xld(SI + 1), y2 = xld(SI + 2);
+    F r;
+    if (i == 0) r = dot(x0, y0, x1, mul_xi<0>(y2), x2, mul_xi<0>(y1));
+    else if (i == 1) r = dot(x0, y1, x1, y0, x2, mul_xi<0>(y2));
+    else r = dot(x0, y2, x1, y1, x2, y0);
+    xst(W_INV + j, r);
+  }
+  team_sync(t);
+}
+
 // wpairing.h final_exp_is_one of the Miller value in slots f0 (unconjugated)
 WVI bool team_final_exp_is_one(Team& t, int f0) {
-  if (t.id == 0) xst_w12(W_INV, w12_inv<true>(xld_w12(f0)));  // conj(f0^-1)
-  team_sync(t);
+  team_w12_inv_conj(t, f0);  // conj(f0^-1)
   team_op(t, W_T, [&](int k) { return w12_mul_c(xld_w12(f0), xld_w12(W_INV), k); });
   team_op(t, W_U, [&](int k) { return w12_frob2_c(xld_w12(W_T), k); });
   team_op(t, W_G, [&](int k) { return w12_mul_c(xld_w12(W_U), xld_w12(W_T), k); });
@@ -400,7 +630,7 @@ WVI bool team_final_exp_is_one(Team& t, int f0) {
   team_op(t, W_U, [&](int k) { return w12_frob2_c(xld_w12(W_C), k); });
   team_op(t, W_P, [&](int k) { return w12_mul_c(xld_w12(W_B), xld_w12(W_U), k); });
   team_op(t, W_A, [&](int k) { return w12_mul_c(xld_w12(W_P), xld_w12(W_C, true), k); });
-  team_op(t, W_U, [&](int k) { return w12_cyc_sqr_c(xld_w12(W_G), k); });
+  team_op_cyc(t, W_U, [&](int k) { return w12_cyc_sqr_c(xld_w12(W_G), k); });
   team_op(t, W_P, [&](int k) { return w12_mul_c(xld_w12(W_A), xld_w12(W_U), k); });
   team_op(t, W_A, [&](int k) { return w12_mul_c(xld_w12(W_P), xld_w12(W_G), k); });
   // e == 1: coefficient k checked by wave k, the six verdicts through scalar words
@@ -426,7 +656,13 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
     // xmd, both SSWU maps and the isogeny on wave 0, the cofactor clearing by the hash team
     Team th = make_team(HASH_TEAM, CTR_HASH);
     WV_PRIO(2);  // above the signature branch's waves on SIMD 1 (wave 5) and the decoder (wave 1)
-    const G2J q = w == 0 ? hash_to_curve_sum(b0) : g2_infinity();
+    // wave 5 multiplies for the SSWU exponentiations of wave 0 (ring_pow_*), wave 4 (on wave 0's
+    // SIMD) stays idle until the cofactor clearing
+    RingCounts rc;
+    G2J q = g2_infinity();
+    if (w == 0) q = hash_to_curve_sum(b0, PowRing{&HASH_RING, &rc});
+    if (w == 5)
+      for (int k = 0; k < SSWU_POWS; k++) ring_pow_consume(HASH_RING, bls::EXP_P_MINUS_3_DIV_4, rc);
     const G2J h = team_clear_cofactor(th, q);
     if (w != 0) WV_PRIO(0);
     if (w == 0) {
@@ -445,7 +681,8 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
   } else if (w == 1) {
     F x, y;
     bool inf;
-    const uint8_t c = g2_decompress(sig, x, y, inf, false);
+    RingCounts rc;
+    const uint8_t c = g2_decompress(sig, x, y, inf, false, PowRing{&SIG_RING, &rc});
     if (c == bls::REJ_OK && !inf) {
       xst(S_SX, x);
       xst(S_SY, y);
@@ -459,6 +696,11 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
     WV_MARK(15);
   } else if ((SIG_TEAM >> w) & 1u) {
     Team t1 = make_team(SIG_TEAM, CTR_SIG);
+    if (w == 2) {  // the decoder's multiplier for its square roots
+      RingCounts rc;
+      for (int k = 0; k < DEC_POWS; k++)
+        if (!ring_pow_consume(SIG_RING, bls::EXP_P_MINUS_3_DIV_4, rc, CTR_DEC)) break;
+    }
     flag_wait(CTR_DEC, 1);
     if (xld_word(XW_CLS) == bls::REJ_OK && !xld_word(XW_SINF)) {
       const MPair m1 = mpair(cst(WC_NEG_G1_X), cst(WC_NEG_G1_Y), xld(S_SX), xld(S_SY));
