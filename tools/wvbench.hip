@@ -14,9 +14,9 @@ __device__ uint64_t g_lat_trace[LAT_TRACE_N];
 }
 using namespace wv;
 
-enum { OP_MULP, OP_DOT1, OP_DOT3, OP_DOT6, OP_SQR2, OP_INV2, OP_INV1, OP_ISZERO, OP_SYNC, OP_TEAM_CYC, OP_TEAM_MUL,
+enum { OP_MULP, OP_SQRP, OP_DOT1, OP_DOT3, OP_DOT6, OP_SQR2, OP_INV2, OP_INV1, OP_ISZERO, OP_SYNC, OP_TEAM_CYC, OP_TEAM_MUL,
        OP_N };
-static const char* NAMES[OP_N] = {"mulp", "dot1", "dot3", "dot6", "sqr2", "inv_pair_nz", "inv_dup", "is_zero2",
+static const char* NAMES[OP_N] = {"mulp", "sqrp", "dot1", "dot3", "dot6", "sqr2", "inv_pair_nz", "inv_dup", "is_zero2",
                                   "team_sync8", "team_cyc_sqr8", "team_mul8"};
 
 __global__ void __launch_bounds__(512) k_wvbench(int op, int six, int iters, uint64_t* out) {
@@ -56,6 +56,7 @@ __global__ void __launch_bounds__(512) k_wvbench(int op, int six, int iters, uin
     for (int i = 0; i < iters; i++) {
       switch (op) {
         case OP_MULP: a = mulp(a, b); break;
+        case OP_SQRP: a = sqrp(a); break;
         case OP_DOT1: a = dot(a, b); break;
         case OP_DOT3: a = dot(a, b, b, a, a, a); break;
         case OP_DOT6: a = dot(a, b, b, a, a, a, b, b, a, b, b, a); break;
