@@ -109,12 +109,13 @@ WVI W12 w12_frob2(const W12& a) {
 
 // Granger-Scott cyclotomic square (tower.h fp12_cyclotomic_sqr) with z0..z5 = c0, c3, c1, c4, c2, c5
 // (w-powers 0, 3, 1, 4, 2, 5): each output is one dot, the 3 t - 2 z / 3 t + 2 z fix-ups as terms
-// against the Montgomery constants -2, 2
+// against the Montgomery constants -2, 2 -- folded into the squared factor where it is the same
+// coefficient (z0' = z0 (3 z0 - 2) + .., z1' = z1 (6 z0 + 2): 2 and 1 terms instead of 3 and 2)
 WVI F w12_cyc_sqr_c(const W12& f, int k) {
   const F &z0 = f.c[0], &z1 = f.c[3], &z2 = f.c[1], &z3 = f.c[4], &z4 = f.c[2], &z5 = f.c[5];
   switch (k) {
-    case 0: return dot(z0, mul_small<3>(z0), z1, mul_small<3>(mul_xi<0>(z1)), z0, cst(WC_NEG2));  // z0' = 3 (z0^2 + xi z1^2) - 2 z0
-    case 3: return dot(z0, mul_small<6>(z1), z1, cst(WC_POS2));                                  // z1' = 6 z0 z1 + 2 z1
+    case 0: return dot(z0, sub<0>(mul_small<3>(z0), cst(WC_POS2)), z1, mul_small<3>(mul_xi<0>(z1)));  // z0' = z0 (3 z0 - 2) + 3 xi z1^2
+    case 3: return dot(z1, add(mul_small<6>(z0), cst(WC_POS2)));                                    // z1' = z1 (6 z0 + 2)
     case 2: return dot(z2, mul_small<3>(z2), z3, mul_small<3>(mul_xi<0>(z3)), z4, cst(WC_NEG2));  // z4' = 3 (z2^2 + xi z3^2) - 2 z4
     case 5: return dot(z2, mul_small<6>(z3), z5, cst(WC_POS2));                                  // z5' = 6 z2 z3 + 2 z5
     case 1: return dot(z4, mul_small<6>(mul_xi<0>(z5)), z2, cst(WC_POS2));                       // z2' = 6 xi z4 z5 + 2 z2

@@ -391,7 +391,7 @@ WVI G2J team_clear_cofactor(Team& t, const G2J& p) {
 }
 
 // ------------------------------------------------------------------ Miller loop of one pair
-// doubling round 1: 0..5 the coefficients of f^2, 6 X^2 -> l2 = 3 X^2 xP, 7 Z^2 -> E = 3 b' Z^2,
+// doubling round 1: 0..5 the coefficients of f^2, 6 X^2 -> l2 = 3 X^2 xP, 7 E = 3 b' Z^2,
 // 8 YZ -> l3 = -2 Y Z yP, 9 A = X Y / 2, 10 B = Y^2 (pairing.h miller_dbl_step)
 WVI void dbl_job1(int j, const MPair& m, int tb, int fin) {
   if (j < 6) {
@@ -401,7 +401,7 @@ WVI void dbl_job1(int j, const MPair& m, int tb, int fin) {
   const F X = xld(tb + TA_TX), Y = xld(tb + TA_TY), Z = xld(tb + TA_TZ);
   switch (j) {
     case 6: xst(tb + TA_L2, mulp(sqr2(X), m.xp3)); break;
-    case 7: xst(tb + TA_E, dot(sqr2(Z), cst(WC_B2X3))); break;
+    case 7: xst(tb + TA_E, dot(Z, mul_small<12>(mul_xi<0>(Z)))); break;  // 3 b' Z^2 with 3 b' = 12 xi: one product
     case 8: {
       const F YZ = dot(Y, Z);
       xst(tb + TA_YZ, YZ);
@@ -432,12 +432,19 @@ WVI void dbl_job2(int j, int tb, int fout) {
     xst(tb + TA_TZ, dot(B, dbl(xld(tb + TA_YZ))));
   }
 }
-// round-1 jobs per wave (bit j = job j): jobs 6, 7, 8 are two products, the rest one
+// round-1 jobs per wave (bit j = job j): jobs 6 and 8 are two products, the rest one
 WVI uint32_t dbl_jobs1(const Team& t) {
   if (t.n == 8) {
-    constexpr uint16_t J8[8] = {(1 << 0) | (1 << 9), (1 << 1) | (1 << 10), (1 << 2) | (1 << 3), 1 << 8,
-                                1 << 4,              1 << 5,               1 << 6,              1 << 7};
+    // the 4-term f^2 outputs (0, 2, 4) and the two-product lines alone, the 3-term outputs each
+    // beside a one-product piece (waves w and w + 4 share a SIMD)
+    constexpr uint16_t J8[8] = {1 << 0, 1 << 2, 1 << 4, 1 << 8, 1 << 6, (1 << 1) | (1 << 9), (1 << 3) | (1 << 10),
+                                (1 << 5) | (1 << 7)};
     return J8[t.id];
+  }
+  if (t.n == 4) {
+    constexpr uint16_t J4[4] = {(1 << 0) | (1 << 1) | (1 << 9), (1 << 2) | (1 << 3) | (1 << 10), (1 << 4) | (1 << 6),
+                                (1 << 5) | (1 << 7) | (1 << 8)};
+    return J4[t.id];
   }
   if (t.n == 5) {
     constexpr uint16_t J5[5] = {(1 << 6) | (1 << 9), (1 << 7) | (1 << 10), (1 << 8) | (1 << 0),
