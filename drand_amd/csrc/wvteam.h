@@ -267,7 +267,7 @@ WVI void team_g2_add_fixed(Team& t, int acc, int base) {
   team_sync(t);
   for (int j = t.id; j < 2; j += t.n) {
     const F r = xld(HS_R), J = xld(HS_J), V = xld(HS_V);
-    if (j == 0) xst(acc, dot(r, r, J, cst(WC_NEG1), V, cst(WC_NEG2)));
+    if (j == 0) xst(acc, dot(r, r, add(J, dbl(V)), cst(WC_NEG1)));  // r^2 - (J + 2V)
     else xst(acc + 1, dot(sub<0>(add(mul_small<3>(V), J), xld(HS_RR)), r, xld(HS_S1), neg<0>(dbl(J))));
   }
   team_sync(t);
@@ -342,7 +342,7 @@ WVI void team_g2_add(Team& t, int acc, int base) {
   team_sync(t);
   for (int j = t.id; j < 2; j += t.n) {
     const F r = xld(HS_R), J = xld(HS_J), V = xld(HS_V);
-    if (j == 0) xst(acc, dot(r, r, J, cst(WC_NEG1), V, cst(WC_NEG2)));
+    if (j == 0) xst(acc, dot(r, r, add(J, dbl(V)), cst(WC_NEG1)));  // r^2 - (J + 2V)
     else xst(acc + 1, dot(sub<0>(add(mul_small<3>(V), J), xld(HS_RR)), r, xld(HS_S1), neg<0>(dbl(J))));
   }
   team_sync(t);
@@ -423,8 +423,7 @@ WVI void dbl_job2(int j, int tb, int fout) {
   }
   const F nE = neg<0>(E);
   if (j == 6) {
-    const F A = xld(tb + TA_A);
-    xst(tb + TA_TX, dot(A, B, mul_small<3>(A), nE));
+    xst(tb + TA_TX, dot(xld(tb + TA_A), sub<1>(B, mul_small<3>(E))));  // A (B - 3E): one product
   } else if (j == 7) {
     const F G = half(add(B, mul_small<3>(E)));
     xst(tb + TA_TY, dot(G, G, mul_small<3>(E), nE));

@@ -86,6 +86,21 @@ def test_generated_history_all_accept(engine, golden, C, n, seg):
         assert C.verify_chained(pk48, fr, prev0, sg[: 8 * 96]) == [0] * min(8, len(sg) // 96)
 
 
+def test_lat_max_clamped_to_one_chunk(engine, golden):
+    """A cut-over above one pipeline chunk is clamped to 2^20 (blsv_set_lat_max, BLSV_LAT_MAX): a
+    call of more items never reaches the latency kernels, whose class buffer is chunk-sized; with the
+    cut-over set huge a 2^20 + 4099-round history still verifies, through the chunked pipeline."""
+    prev = engine.set_lat_max(1 << 40)
+    try:
+        assert engine.set_lat_max(1 << 40) == 1 << 20
+        n, seg = 1 << 20 | 4099, 64
+        seeds, sigs, s0 = _history(engine, golden, n, seg, seed=5)
+        ok, fb, cls = _verify(engine, 1, seg, seeds, s0, sigs, n)
+        assert all(ok) and fb == NONE and not any(cls)
+    finally:
+        engine.set_lat_max(prev)
+
+
 def test_corrupted_history_rejects_exactly(engine, golden, C):
     import torch
 
