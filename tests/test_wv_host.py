@@ -72,6 +72,16 @@ def test_lane_gcd_inverse(wvtest):
         assert [int(x, 16) for x in line.split()] == [want, want], hex(v)
 
 
+def test_team_g2_addition_cases(wvtest, golden):
+    """wvteam.h team_g2_add (the hash team's five-round G2 addition, three host threads) against the
+    one-wave wcurve.h g2_add on the cases a hash never reaches: P + P (doubling), P + (-P) (infinity),
+    O + Q, Q + O, besides a generic sum; and the team [|x|] chain (team_mul_x_abs) against
+    g2_mul_x_abs -- on golden signature points in scaled Jacobian coordinates."""
+    sigs = [golden["kat"]["sig"]] + [b["sig"] for b in golden["chained"]["beacons"][:2]]
+    lines = ["%s %s" % (s, c) for s in sigs for c in ("sum", "dbl", "neg", "ainf", "binf", "chain")]
+    assert run(wvtest, "teamadd", lines) == ["ok"] * len(lines)
+
+
 def test_hash_to_g2_golden(wvtest, golden):
     cases = golden["hash_to_g2"]
     out = run(wvtest, "hash", [h["msg"] or "-" for h in cases])

@@ -4,6 +4,7 @@
 //
 // usage: wvtest field   < lines "a0 a1 b0 b1" (hex, raw values < p)  -> one line of results each
 //        wvtest inv     < lines "a" (hex, raw < p)                    -> raw a^-1 in both halves (lane GCD)
+//        wvtest teamadd < lines "sig96 case"                          -> ok / bad (team G2 addition)
 //        wvtest verify  < lines "pk48 msg sig96" (hex)                -> reject class per line
 //        wvtest hash    < lines "msg" (hex)                            -> affine H(msg) raw hex
 //        wvtest pair    < lines "px py qx0 qx1 qy0 qy1" (affine raw)  -> Miller loop + final exp (raw)
@@ -289,9 +290,57 @@ static int cmd_smul() {
   return 0;
 }
 
+// teamadd: "sig96 case" -> ok / bad: wvteam.h team_g2_add (three host threads as the hash team's
+// waves 0, 4, 5) against wcurve.h g2_add for case sum (P' + 2P), dbl (P' + P), neg (P' + (-P)),
+// ainf (O + 2P), binf (P' + O), with P' = P in scaled Jacobian coordinates (Z = x_P); and "chain"
+// (team_mul_x_abs against g2_mul_x_abs on P')
+static int cmd_teamadd() {
+  char a[300], b[32];
+  while (scanf("%299s %31s", a, b) == 2) {
+    wv_init();
+    const auto sig = unhex(a);
+    F x, y;
+    bool inf;
+    if (g2_decompress(sig.data(), x, y, inf) || inf) {
+      printf("-\n");
+      continue;
+    }
+    const G2J p = {x, y, cst(WC_ONE2)};
+    const F l2 = sqr2(x);
+    const G2J ps = {dot(p.x, l2), dot(p.y, dot(l2, x)), dot(p.z, x)};
+    const G2J p2 = g2_dbl(p);
+    const std::string c(b);
+    G2J A = ps, B = p2;
+    if (c == "dbl") B = p;
+    else if (c == "neg") B = g2_neg(p);
+    else if (c == "ainf") A = g2_infinity();
+    else if (c == "binf") B = g2_infinity();
+    const bool chain = c == "chain";
+    const G2J want = chain ? g2_mul_x_abs(ps) : g2_add(A, B);
+    for (auto& ctr : g_host_ctr) ctr.store(0);
+    xst_g2(HS_ACC, chain ? ps : A);
+    xst_g2(HS_Q2, chain ? ps : B);
+    std::thread th[3];
+    const int waves[3] = {0, 4, 5};
+    for (int k = 0; k < 3; k++)
+      th[k] = std::thread([&, k]() {
+        g_host_wave = waves[k];
+        wv_init();
+        Team t = make_team(HASH_TEAM, CTR_HASH);
+        if (chain) team_mul_x_abs(t, HS_Q2, HS_ACC);
+        else team_g2_add(t, HS_ACC, HS_Q2);
+      });
+    for (auto& t : th) t.join();
+    printf("%s\n", g2_eq(xld_g2(HS_ACC), want) ? "ok" : "bad");
+    fflush(stdout);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 2 && !strcmp(argv[1], "field")) return cmd_field();
   if (argc >= 2 && !strcmp(argv[1], "inv")) return cmd_inv();
+  if (argc >= 2 && !strcmp(argv[1], "teamadd")) return cmd_teamadd();
   if (argc >= 2 && !strcmp(argv[1], "verify")) return cmd_verify();
   if (argc >= 2 && !strcmp(argv[1], "tverify")) return cmd_tverify();
   if (argc >= 2 && !strcmp(argv[1], "hash")) return cmd_hash();
