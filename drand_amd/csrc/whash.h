@@ -111,33 +111,65 @@ struct PowSelf {
   WVI F operator()(const F& a) const { return pow_pm3d4(a); }
 };
 
+// The affine side of the two SSWU maps: x1 = xN / xD and gx1 = (x1^2 + A) x1 + B from the projective
+// xN, xD and the pair of norms N(xD) (inverted as one pair). sswu2 needs it only after the first
+// exponentiation, so the team form runs it on another wave meanwhile (wvteam.h).
+struct SswuAff {
+  F ndi, x1[2], gx1[2];
+};
+WVI SswuAff sswu_affine(const F& nd, const F (&xN)[2], const F (&xD)[2]) {
+  const F A = cst(WC_SSWU_A), B = cst(WC_SSWU_B), one = cst(WC_ONE2);
+  SswuAff r;
+  r.ndi = inv_pair_nz(nd);
+  for (int m = 0; m < 2; m++) {
+    const F ni = m == 0 ? dup0(r.ndi) : dup1(r.ndi);
+    r.x1[m] = dot(xN[m], mulp(conj<0>(xD[m]), ni));                        // xN conj(xD) / N(xD)
+    r.gx1[m] = dot(dot(sqr2(r.x1[m]), one, A, one), r.x1[m], B, one);     // (x^2 + A) x + B
+  }
+  return r;
+}
+// ... on this wave, when sswu2 asks for it
+struct AffSelf {
+  F nd, xN[2], xD[2];
+  WVI void start(const F& n, const F (&a)[2], const F (&b)[2]) {
+    nd = n;
+    for (int m = 0; m < 2; m++) xN[m] = a[m], xD[m] = b[m];
+  }
+  WVI SswuAff get() const { return sswu_affine(nd, xN, xD); }
+};
+
 // both SSWU maps of a hash: (x_m, y_m) on E2' for u_m (hash.h map_to_curve_sswu with its tv1); pw
-// computes a^((p-3)/4) per half
-template <class Pow = PowSelf>
-WVI void sswu2(const F (&u)[2], F (&xo)[2], F (&yo)[2], Pow pw = Pow()) {
-  const F Z = cst(WC_SSWU_Z), A = cst(WC_SSWU_A), B = cst(WC_SSWU_B);
+// computes a^((p-3)/4) per half. The first exponentiation (the root of N(gx1), whether gx1 is a
+// square) runs on the projective x1 = xN / xD: N(gx1) = N(gxN) / N(xD)^3 = n' / N(xD)^4 with
+// n' = N(gxN) N(xD), so its root is the root of n' times N(xD)^-2 and n' is a square exactly when
+// N(gx1) is; the inversion and the affine x1, gx1 (aff) are needed only after it.
+template <class Pow = PowSelf, class Aff = AffSelf>
+WVI void sswu2(const F (&u)[2], F (&xo)[2], F (&yo)[2], Pow pw = Pow(), Aff aff = Aff()) {
+  const F Z = cst(WC_SSWU_Z), A = cst(WC_SSWU_A), B = cst(WC_SSWU_B), one = cst(WC_ONE2);
   F zu2[2], den[2];
-  uint32_t dz = 0;
   for (int m = 0; m < 2; m++) {
     zu2[m] = dot(sqr2(u[m]), Z);
-    den[m] = dot(zu2[m], zu2[m], zu2[m], cst(WC_ONE2));  // Z^2 u^4 + Z u^2
+    den[m] = dot(zu2[m], zu2[m], zu2[m], one);  // Z^2 u^4 + Z u^2
   }
-  // tv1 = inv0(den) = conj(den) / N(den): the two norms inverted as one pair
-  const F nd = select_halves(1u, norm_dup(den[0]), norm_dup(den[1]));
-  dz = zero_halves(nd);
-  const F ndi = inv_pair_nz(select_halves(dz, cst(WC_ONE_DUP), nd));  // zero norms replaced by 1
-  F gx1[2], x1[2];
+  const F ndr = select_halves(1u, norm_dup(den[0]), norm_dup(den[1]));
+  const uint32_t dz = zero_halves(ndr);
+  // x1 = xN / xD: xN = -B/A (den + 1), xD = den; den = 0: x1 = B / (Z A), xD = 1
+  F xN[2], xD[2], gxN[2];
   for (int m = 0; m < 2; m++) {
     const bool z = (dz >> m) & 1u;
-    const F ni = m == 0 ? dup0(ndi) : dup1(ndi);
-    const F tv1 = z ? zero() : mulp(conj<0>(den[m]), ni);
-    x1[m] = z ? cst(WC_SSWU_BZA) : dot(cst(WC_SSWU_NBA), tv1, cst(WC_SSWU_NBA), cst(WC_ONE2));  // -B/A (1 + tv1)
-    gx1[m] = dot(dot(sqr2(x1[m]), cst(WC_ONE2), A, cst(WC_ONE2)), x1[m], B, cst(WC_ONE2));        // (x^2 + A) x + B
+    xD[m] = z ? one : den[m];
+    xN[m] = z ? cst(WC_SSWU_BZA) : dot(cst(WC_SSWU_NBA), den[m], cst(WC_SSWU_NBA), one);
+    const F xD2 = sqr2(xD[m]);
+    gxN[m] = dot(dot(sqr2(xN[m]), one, A, xD2), xN[m], B, dot(xD[m], xD2));  // (xN^2 + A xD^2) xN + B xD^3
   }
-  // root of the norms: w = n^((p-3)/4), r1 = w n; sq1 = r1^2 == n (N(gx1) a square)
-  const F n = select_halves(1u, norm_dup(gx1[0]), norm_dup(gx1[1]));
-  const F r1 = mulp(pw(n), n);
-  const uint32_t sq1 = zero_halves(sub<0>(sqrp(r1), n));
+  const F nd = select_halves(dz, cst(WC_ONE_DUP), ndr);  // N(xD)
+  aff.start(nd, xN, xD);
+  const F np = mulp(select_halves(1u, norm_dup(gxN[0]), norm_dup(gxN[1])), nd);
+  const F r1p = mulp(pw(np), np);
+  const uint32_t sq1 = zero_halves(sub<0>(sqrp(r1p), np));
+  const SswuAff af = aff.get();
+  // r1: a root of N(gx1) when it is a square (r1^2 = -N(gx1) otherwise, as with the direct form)
+  const F r1 = mulp(r1p, sqrp(af.ndi));
   // r2 = N(u)^3 sqrt(-N(Z)^3) r1 (the root for gx2 = (Z u^2)^3 gx1 when N(gx1) is not a square)
   const F nu = select_halves(1u, norm_dup(u[0]), norm_dup(u[1]));
   const F r2 = mulp(mulp(mulp(sqrp(nu), nu), cst(WC_SSWU_SQRT_MNZ3)), r1);
@@ -145,9 +177,9 @@ WVI void sswu2(const F (&u)[2], F (&xo)[2], F (&yo)[2], Pow pw = Pow()) {
   F gx[2];
   for (int m = 0; m < 2; m++) {
     const bool q = (sq1 >> m) & 1u;
-    const F x2 = dot(zu2[m], x1[m]);
-    xo[m] = q ? x1[m] : x2;
-    gx[m] = q ? gx1[m] : dot(dot(sqr2(zu2[m]), zu2[m]), gx1[m]);
+    const F x2 = dot(zu2[m], af.x1[m]);
+    xo[m] = q ? af.x1[m] : x2;
+    gx[m] = q ? af.gx1[m] : dot(dot(sqr2(zu2[m]), zu2[m]), af.gx1[m]);
   }
   // sqrt of gx through the norm root s (tower.h fp2_sqrt_with_norm_root), both maps, both
   // candidates (a0 + s)/2 and (a0 - s)/2 -- per map the second replaces the first when it is 0
@@ -188,14 +220,14 @@ WVI G2J iso_map(const F& x, const F& y) {
 }
 
 // the sum of the two mapped points (before the cofactor clearing) from the message's xmd b_0
-template <class Pow = PowSelf>
-WVI G2J hash_to_curve_sum(const uint32_t (&b0)[8], Pow pw = Pow()) {
+template <class Pow = PowSelf, class Aff = AffSelf>
+WVI G2J hash_to_curve_sum(const uint32_t (&b0)[8], Pow pw = Pow(), Aff aff = Aff()) {
   uint32_t e[4][16];
   xmd_words(b0, e);
   const F u[2] = {fp2_from_be512(e[0], e[1]), fp2_from_be512(e[2], e[3])};
   F x[2], y[2];
   WV_MARK(10);
-  sswu2(u, x, y, pw);
+  sswu2(u, x, y, pw, aff);
   WV_MARK(11);
   const G2J q = g2_add(iso_map(x[0], y[0]), iso_map(x[1], y[1]));
   WV_MARK(12);

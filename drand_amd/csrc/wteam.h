@@ -24,7 +24,7 @@ namespace wv {
 #define WV_BLK_SLOTS 128
 #endif
 constexpr int BLK_SLOTS = WV_BLK_SLOTS;
-constexpr int BLK_CTRS = 12;  // team counters
+constexpr int BLK_CTRS = 16;  // team counters
 constexpr int BLK_WORDS_EXTRA = 64;  // scalar words (verdicts, flags)
 
 #ifdef WV_HOST

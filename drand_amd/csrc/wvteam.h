@@ -1,9 +1,11 @@
 // One verification by a team of eight waves (two per SIMD of a CU), the latency engine's device form
 // (k_lat.hip). The work of wverify.h's verify_item, scheduled across the waves:
 //
-//   phase A  wave 0: hash-to-G2 of the message at raised issue priority, wave 5 multiplying for its two
-//            SSWU exponentiations (ring_pow_*); waves 4, 5 join it for the cofactor clearing (team_clear_cofactor: each doubling in three rounds, each chain
-//            addition in five)
+//   phase A  wave 0: hash-to-G2 of the message at raised issue priority: wave 5 multiplies for its
+//            two SSWU square roots (ring_pow_*) and then maps the second point through the isogeny,
+//            wave 3 computes the SSWU inversion and the affine x1, gx1 beside the first root
+//            (aff_serve), waves 4 and 5 join it for the cofactor
+//            clearing (team_clear_cofactor: each doubling in three rounds, each addition in five)
 //            wave 1: decompression of the signature (wave 2 multiplying for its square roots), then
 //            its subgroup check
 //            waves 2, 3, 6, 7: as soon as wave 1 has the point, the Miller loop of the signature
@@ -190,6 +192,68 @@ struct PowRing {
   WVI F operator()(const F& a) const { return ring_pow_produce(*rg, a, bls::EXP_P_MINUS_3_DIV_4, *rc); }
 };
 constexpr int SSWU_POWS = 2;  // whash.h sswu2: the norms' root, then the candidates' root
+
+// SSWU's affine side (whash.h sswu_affine: the pair inversion, x1 and gx1 of both maps) on a helper
+// wave while the hash wave runs its first exponentiation: the request (N(xD), xN, xD) and the
+// answer (1 / N(xD), x1, gx1) through slots of the key pair's area beside the ring
+constexpr int AFF_Q = TB0 + 10, AFF_A = TB0 + 15, CTR_AFQ = 7, CTR_AFA = 11;
+struct AffTeam {
+  WVI void start(const F& nd, const F (&xN)[2], const F (&xD)[2]) const {
+    xst(AFF_Q, nd);
+    for (int m = 0; m < 2; m++) {
+      xst(AFF_Q + 1 + m, xN[m]);
+      xst(AFF_Q + 3 + m, xD[m]);
+    }
+    flag_post_lds(CTR_AFQ);
+  }
+  WVI SswuAff get() const {
+    flag_wait(CTR_AFA, 1);
+    SswuAff r;
+    r.ndi = xld(AFF_A);
+    for (int m = 0; m < 2; m++) {
+      r.x1[m] = xld(AFF_A + 1 + m);
+      r.gx1[m] = xld(AFF_A + 3 + m);
+    }
+    return r;
+  }
+};
+// the second map's isogeny on wave 5 (after its ring products) beside the first map's on wave 0
+constexpr int ISO_Q = TB0 + 20, ISO_A = TB0 + 22, CTR_ISOQ = 12, CTR_ISOA = 13;
+// wave 0's hash up to the sum of the two mapped points (whash.h hash_to_curve_sum, the team form)
+WVI G2J team_hash_to_curve_sum(const uint32_t (&b0)[8], RingCounts& rc) {
+  uint32_t e[4][16];
+  xmd_words(b0, e);
+  const F u[2] = {fp2_from_be512(e[0], e[1]), fp2_from_be512(e[2], e[3])};
+  F x[2], y[2];
+  WV_MARK(10);
+  sswu2(u, x, y, PowRing{&HASH_RING, &rc}, AffTeam{});
+  WV_MARK(11);
+  xst(ISO_Q, x[1]);
+  xst(ISO_Q + 1, y[1]);
+  flag_post_lds(CTR_ISOQ);
+  const G2J q0 = iso_map(x[0], y[0]);
+  flag_wait(CTR_ISOA, 1);
+  const G2J q = g2_add(q0, xld_g2(ISO_A));
+  WV_MARK(12);
+  return q;
+}
+WVI void iso_serve() {
+  flag_wait(CTR_ISOQ, 1);
+  xst_g2(ISO_A, iso_map(xld(ISO_Q), xld(ISO_Q + 1)));
+  flag_post(CTR_ISOA);
+}
+
+WVI void aff_serve() {
+  flag_wait(CTR_AFQ, 1);
+  const F xN[2] = {xld(AFF_Q + 1), xld(AFF_Q + 2)}, xD[2] = {xld(AFF_Q + 3), xld(AFF_Q + 4)};
+  const SswuAff r = sswu_affine(xld(AFF_Q), xN, xD);
+  xst(AFF_A, r.ndi);
+  for (int m = 0; m < 2; m++) {
+    xst(AFF_A + 1 + m, r.x1[m]);
+    xst(AFF_A + 3 + m, r.gx1[m]);
+  }
+  flag_post(CTR_AFA);
+}
 constexpr int DEC_POWS = 2;   // whash.h g2_decompress (none when it rejects before its square root)
 
 // ------------------------------------------------------------------ cofactor clearing by a team
@@ -666,9 +730,11 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
     // SIMD) stays idle until the cofactor clearing
     RingCounts rc;
     G2J q = g2_infinity();
-    if (w == 0) q = hash_to_curve_sum(b0, PowRing{&HASH_RING, &rc});
-    if (w == 5)
+    if (w == 0) q = team_hash_to_curve_sum(b0, rc);
+    if (w == 5) {
       for (int k = 0; k < SSWU_POWS; k++) ring_pow_consume(HASH_RING, bls::EXP_P_MINUS_3_DIV_4, rc);
+      iso_serve();
+    }
     const G2J h = team_clear_cofactor(th, q);
     if (w != 0) WV_PRIO(0);
     if (w == 0) {
@@ -702,6 +768,7 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
     WV_MARK(15);
   } else if ((SIG_TEAM >> w) & 1u) {
     Team t1 = make_team(SIG_TEAM, CTR_SIG);
+    if (w == 3) aff_serve();  // the hash's SSWU inversion and affine x1, gx1, idle time of this team
     if (w == 2) {  // the decoder's multiplier for its square roots
       RingCounts rc;
       for (int k = 0; k < DEC_POWS; k++)
