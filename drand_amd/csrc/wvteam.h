@@ -19,7 +19,7 @@
 // T pieces (X^2 -> l2, Z^2 -> E, YZ -> l3, A, B), (2) the six coefficients of f^2 l and T's new X, Y,
 // Z; an addition step is four rounds of one-product jobs. Every Fp12 operation of the final
 // exponentiation gives its six output coefficients to six waves. Two waves per SIMD each run at ~0.8
-// of a lone wave's pace (profiles/r04m_latency_sweep.json: 512 teams of four on 256 CUs take 1.21x
+// of a lone wave's pace (profiles/r04m_latency_sweep_4wave.log: 512 teams of four on 256 CUs take 1.21x
 // the time of 256), so halving the rounds of a step pays.
 #pragma once
 #include "wteam.h"
