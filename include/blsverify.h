@@ -26,9 +26,9 @@
  * VerifyPartial, chain/beacon/node.go:112,125; identity checks, key/keys.go:60-63)
  *  - A call with at most lat_max items (blsv_set_lat_max, default 1024) runs on the LATENCY path: one
  *    workgroup of eight waves per item, every limb of a field element in its own lane
- *    (drand_amd/csrc/k_lat.hip). Measured on MI355X (profiles/r04zf_latency.json and
- *    r04zf_cabi_smoke.txt, this ABI from plain C, warm): one VerifyRecovered 2.4 ms; blsv_aggregate
- *    of an n = 64 / t = 33 round (64 VerifyPartial + Recover + VerifyRecovered) 6.9-7.0 ms. Up to 256 items the time stays ~3.3 ms (every item has its
+ *    (drand_amd/csrc/k_lat.hip). Measured on MI355X (profiles/r04zi_latency.json, warm): one
+ *    VerifyRecovered 2.3 ms; blsv_aggregate of an n = 64 / t = 33 round (64 VerifyPartial +
+ *    Recover + VerifyRecovered) 6.8 ms. Up to 256 items the time stays ~3.3 ms (every item has its
  *    own CU), then grows ~3.3 ms per further 256 items (profiles/r04n_latency_sweep.json).
  *  - Larger calls run on the BATCH pipeline (one lane per item, staged kernels): ~19 ms floor, then
  *    ~0.5 us per item (about 2 M items/s). Both paths give identical verdicts, reject classes and
