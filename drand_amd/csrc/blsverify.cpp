@@ -62,7 +62,7 @@ struct ProfRec {
 // of at most this many items runs on the latency path. BLSV_LAT_MAX overrides it (0 = batch pipeline
 // only). Any value is clamped to kMaxChunk: the latency kernels write one class byte per item into the
 // chunk-sized class buffer, so a larger batch always takes the chunked pipeline.
-constexpr size_t kLatMaxDefault = 1024;  // profiles/r04n_latency_sweep.json: 8-wave teams, one per CU
+constexpr size_t kLatMaxDefault = 1536;  // profiles/r04zk_latency_sweep.json: the paths cross near 1,750
 static size_t lat_max_env() {
   static const size_t v = [] {
     const char* e = getenv("BLSV_LAT_MAX");

@@ -24,12 +24,12 @@
  * Latency contract (single-item and small callers: client.Get's per-round verify,
  * client/verify.go:185-207; the gossip validator, lp2p/client/validator.go:64; per-packet
  * VerifyPartial, chain/beacon/node.go:112,125; identity checks, key/keys.go:60-63)
- *  - A call with at most lat_max items (blsv_set_lat_max, default 1024) runs on the LATENCY path: one
+ *  - A call with at most lat_max items (blsv_set_lat_max, default 1536) runs on the LATENCY path: one
  *    workgroup of eight waves per item, every limb of a field element in its own lane
  *    (drand_amd/csrc/k_lat.hip). Measured on MI355X (profiles/r04zi_latency.json, warm): one
  *    VerifyRecovered 2.3 ms; blsv_aggregate of an n = 64 / t = 33 round (64 VerifyPartial +
- *    Recover + VerifyRecovered) 6.8 ms. Up to 256 items the time stays ~3.3 ms (every item has its
- *    own CU), then grows ~3.3 ms per further 256 items (profiles/r04n_latency_sweep.json).
+ *    Recover + VerifyRecovered) 6.8 ms. Up to 256 items the time stays ~2.5 ms (every item has its
+ *    own CU), then grows ~2.35 ms per further 256 items (profiles/r04zk_latency_sweep.json).
  *  - Larger calls run on the BATCH pipeline (one lane per item, staged kernels): ~19 ms floor, then
  *    ~0.5 us per item (about 2 M items/s). Both paths give identical verdicts, reject classes and
  *    recovered bytes (tests/test_gpu_lat.py runs the same vectors through both).
@@ -234,7 +234,7 @@ int blsv_synchronize(blsv_ctx* ctx);
  * Latency-path cutover (see the latency contract above): calls with 1..lat_max items take the latency
  * path, larger ones the batch pipeline; 0 = batch pipeline only. The default is the BLSV_LAT_MAX
  * environment variable (a non-negative decimal integer; anything else is ignored with a warning on
- * stderr), else 1024 (below where the two paths cross on MI355X, ~1,250 items). Values above 2^20 (one pipeline chunk)
+ * stderr), else 1536 (below where the two paths cross on MI355X, ~1,750 items). Values above 2^20 (one pipeline chunk)
  * are clamped to 2^20. Returns the previous value.
  */
 size_t blsv_set_lat_max(blsv_ctx* ctx, size_t lat_max);

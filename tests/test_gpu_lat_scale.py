@@ -1,6 +1,6 @@
 """Parity of the latency path at the sizes it serves.
 
-Every host call of 1..lat_max items (default 1,024) runs on the latency engine (k_lat.hip: one
+Every host call of 1..lat_max items (default 1,536) runs on the latency engine (k_lat.hip: one
 workgroup per item, limbs across lanes), a second implementation of the arithmetic beside the batch
 pipeline (one lane per item). This file puts full-size batches through the DEFAULT routing and checks
 them three ways: against the same call forced onto the batch pipeline (set_lat_max(0)), forced onto
@@ -8,7 +8,7 @@ the latency path, and against the C oracle's reject classes (oracle/c/bls_oracle
 reference KAT) at every injected position and its successor:
 
   * a continuous 2,049-round chained history (tests/golden/chain2049.bin, make_chain_fixture.py)
-    through host verify_chained at n = 1,000 (configs[0]), 1,024 (= lat_max), 1,025 (= lat_max + 1,
+    through host verify_chained at n = 1,000 (configs[0]), 1,536 (= lat_max), 1,537 (= lat_max + 1,
     the batch side of the cut-over) and 2,048, with every class of the mixed golden injected at the first, a
     middle, the last item and a 64-item edge (client/verify.go:146-163, chain/beacon.go:87-108);
   * the same through blsv_verify_prevs (stored PreviousSig per row: the drand.db loader's call);
@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NONE = (1 << 64) - 1
 BIG = 1 << 20
-LAT_MAX = 1024  # blsverify.cpp kLatMaxDefault (test_default_cutover)
+LAT_MAX = 1536  # blsverify.cpp kLatMaxDefault (test_default_cutover)
 
 # classes of the mixed golden (tests/golden/golden.json "mixed"): name -> source index there; the
 # decode classes are copied as bytes, the others are made from the local signature
