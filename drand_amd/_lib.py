@@ -81,6 +81,14 @@ SIGNATURES = {
     "blsv_test_hash_to_g2": (ctypes.c_int, [vp, u8p, u32p, sz, u32p, u8p]),
     "blsv_test_final_exp": (ctypes.c_int, [vp, u32p, sz, u32p, u32p]),
     "blsv_set_lat_max": (sz, [vp, sz]),
+    "blsv_set_chunk": (sz, [vp, sz]),
+    "blsv_workspace_bytes": (sz, [vp]),
+    "blsv_lat_trace_enable": (ctypes.c_int, [vp, ctypes.c_int]),
+    "blsv_service_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(vp)]),
+    "blsv_service_destroy": (None, [vp]),
+    "blsv_service_verify_partial": (ctypes.c_int, [vp, u8p, sz, sz, u8p, sz, u8p, sz, u8p, u8p]),
+    "blsv_service_verify_recovered": (ctypes.c_int, [vp, u8p, u8p, sz, u8p, u8p, u8p]),
+    "blsv_service_stats": (ctypes.c_int, [vp, u64p, u64p, u64p]),
 }
 
 _lib = None

@@ -18,7 +18,8 @@ import numpy as np
 
 from .callers import _verify_run
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libboltload.so")
+LIB_PATH = os.environ.get("DRAND_AMD_BOLTLOAD_LIB",
+                          os.path.join(os.path.dirname(os.path.abspath(__file__)), "libboltload.so"))
 _lib = None
 
 

@@ -15,139 +15,46 @@
 #include "../../include/blsverify.h"
 #include "../../include/blsverify_testing.h"
 #include "kernels.h"
+#include "engine_ctx.h"
 
-namespace {
-
-constexpr size_t kMaxChunk = size_t(1) << 20;  // beacons per pipeline pass (~1 GB of staging)
-// Miller line staging holds a whole chunk: 1 Mi beacons x 39 KB = 41 GB of the 288 GB. Same-box A/B
-// (profiles/r04k_line_sub_ab.json): 128 Ki sub-chunks 216.9 ms, 256 Ki 215.8, the whole chunk 210.7 per 1M
-// (one lines + one f launch instead of eight of each, so one wave tail instead of eight).
-constexpr size_t kLineSub = kMaxChunk;
-
-struct DBuf {
-  void* p = nullptr;
-  size_t sz = 0;
-  ~DBuf() {
-    if (p) (void)hipFree(p);
-  }
-  hipError_t ensure(size_t need) {
-    if (need <= sz) return hipSuccess;
-    if (p) {
-      (void)hipFree(p);
-      p = nullptr;
-      sz = 0;
-    }
-    size_t want = std::max(need, size_t(256));
-    hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) sz = want;
-    return e;
-  }
-  template <typename T>
-  T* as() const {
-    return static_cast<T*>(p);
-  }
-};
-
-}  // namespace
-
-// Stage timing (blsv_profile_*): HIP events recorded around every stage launch on the launch stream.
-enum Stage { ST_HASH = 0, ST_DECOMP = 1, ST_MILLER = 2, ST_FEXP = 3, ST_FINISH = 4, ST_LAT = 5, ST_N = 6 };
-struct ProfRec {
-  int stage;
-  size_t items;
-  hipEvent_t a, b;
-};
-
-// Cutover between the latency path (one workgroup per item, k_lat.hip) and the batch pipeline: a batch
-// of at most this many items runs on the latency path. BLSV_LAT_MAX overrides it (0 = batch pipeline
-// only). Any value is clamped to kMaxChunk: the latency kernels write one class byte per item into the
-// chunk-sized class buffer, so a larger batch always takes the chunked pipeline.
-constexpr size_t kLatMaxDefault = 1536;  // profiles/r04zk_latency_sweep.json: the paths cross near 1,750
-static size_t lat_max_env() {
-  static const size_t v = [] {
-    const char* e = getenv("BLSV_LAT_MAX");
-    if (!e) return kLatMaxDefault;
-    char* end = nullptr;
-    errno = 0;
-    const unsigned long long x = strtoull(e, &end, 10);
-    if (end == e || *end != '\0' || errno == ERANGE || e[0] == '-') {
-      fprintf(stderr, "blsverify: ignoring BLSV_LAT_MAX=\"%s\" (not a non-negative integer); cutover stays %zu\n", e,
-              kLatMaxDefault);
-      return kLatMaxDefault;
-    }
-    return (size_t)std::min<unsigned long long>(x, kMaxChunk);
-  }();
-  return v;
+void release_workspace(blsv_ctx* c) {
+  for (DBuf* d : {&c->H, &c->HQ, &c->S, &c->F, &c->FW, &c->LN, &c->h_inf, &c->s_inf, &c->cls}) d->release();
+  c->cap = 0;
 }
 
-struct blsv_ctx {
-  int device = 0;
-  bool prof = false;
-  size_t lat_max = lat_max_env();
-  std::vector<ProfRec> recs;
-  std::vector<hipEvent_t> event_pool;
-  hipStream_t stream = nullptr;
-  // decompression runs beside hash-to-G2 (they are independent): a side stream forked from and
-  // joined back into the launch stream with these two events
-  hipStream_t side = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  std::string err;
-  // group
-  bool has_group = false;
-  size_t t = 0, n = 0;
-  DBuf commits, commit_inf;
-  std::vector<uint8_t> group_bytes;  // the commitments of the current group (set_group is a no-op on a repeat)
-  // PubPoly.Eval(i) for every share index i < min(n, kPkTable), computed once per group on its first
-// partials call; indices beyond the table are evaluated per batch
-  DBuf pk_all, pk_all_inf;
-  size_t pk_all_n = 0;
-  bool pk_all_built = false;
-  // explicit-pk override (verify_messages with pk48)
-  DBuf pk_tab, pk_inf;
-  uint8_t pk_cache[48];
-  bool pk_cache_valid = false;
-  // staging workspace
-  size_t cap = 0;
-  DBuf H, S, F, FW, LN, h_inf, s_inf, cls;
-  DBuf HQ;  // hash-to-G2 phase staging (kernels.h HQ_WORDS per item)
-  // inputs / outputs
-  DBuf in_sigs, in_msgs, in_off, in_len, in_rounds, seeds, bitmap, first_bad, sk, idx, lambdas, scratch, out,
-      pp_tab, pp_inf, sel, g1_cls, misc;
-};
-
-#define HIPCHK(ctx, expr)                                                             \
-  do {                                                                                \
-    hipError_t e_ = (expr);                                                           \
-    if (e_ != hipSuccess) return fail((ctx), BLSV_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
-  } while (0)
-
-static int fail(blsv_ctx* ctx, int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  if (ctx) ctx->err = buf;
-  return code;
-}
-
-static int ensure_workspace(blsv_ctx* c, size_t cnt) {
-  size_t want = std::min(std::max(cnt, size_t(64)), kMaxChunk);
-  want = (want + 63) & ~size_t(63);
-  if (want <= c->cap) return BLSV_OK;
-  HIPCHK(c, c->H.ensure(want * blsk::H_WORDS * 4));
-  HIPCHK(c, c->HQ.ensure(want * blsk::HQ_WORDS * 4));
-  HIPCHK(c, c->S.ensure(want * blsk::S_WORDS * 4));
-  HIPCHK(c, c->F.ensure(want * blsk::F_WORDS * 4));
-  HIPCHK(c, c->FW.ensure(3 * want * blsk::F_WORDS * 4));
-  HIPCHK(c, c->LN.ensure(std::max(std::min(want, kLineSub) * blsk::MILLER_LINE_WORDS,
-                                   blsk::FEXP_PARK_WORDS(want)) * 4));  // LN doubles as the final exp's park
-  static_assert(3 * blsk::F_WORDS >= 48 * 64 / 21 + 1, "FW holds the Miller park of a sub-chunk");
-  HIPCHK(c, c->h_inf.ensure(want));
-  HIPCHK(c, c->s_inf.ensure(want));
-  HIPCHK(c, c->cls.ensure(want));
-  c->cap = want;
-  return BLSV_OK;
+int ensure_workspace(blsv_ctx* c, size_t cnt) {
+  for (;;) {
+    size_t want = std::min(std::max(cnt, size_t(64)), c->chunk);
+    want = (want + 63) & ~size_t(63);
+    if (want <= c->cap) return BLSV_OK;
+    hipError_t e = hipSuccess;
+    auto need = [&](DBuf& d, size_t bytes) {
+      if (e == hipSuccess) e = d.ensure(bytes);
+    };
+    need(c->H, want * blsk::H_WORDS * 4);
+    need(c->HQ, want * blsk::HQ_WORDS * 4);
+    need(c->S, want * blsk::S_WORDS * 4);
+    need(c->F, want * blsk::F_WORDS * 4);
+    need(c->FW, 3 * want * blsk::F_WORDS * 4);
+    // LN doubles as the final exponentiation's park
+    need(c->LN, std::max(std::min(want, kLineSub) * blsk::MILLER_LINE_WORDS, blsk::FEXP_PARK_WORDS(want)) * 4);
+    need(c->h_inf, want);
+    need(c->s_inf, want);
+    need(c->cls, want);
+    static_assert(3 * blsk::F_WORDS >= 48 * 64 / 21 + 1, "FW holds the Miller park of a sub-chunk");
+    if (e == hipSuccess) {
+      c->cap = want;
+      return BLSV_OK;
+    }
+    release_workspace(c);
+    (void)hipGetLastError();  // clear the sticky allocation error
+    if (e != hipErrorOutOfMemory || want <= kMinChunk)
+      return fail(c, BLSV_EHIP, "staging for %zu items: %s", want, hipGetErrorString(e));
+    // out of HBM (other contexts or ranks on this GPU): halve the pass size and retry
+    c->chunk = std::max(kMinChunk, ((want / 2) + 63) & ~size_t(63));
+    c->lat_max = std::min(c->lat_max, c->chunk);
+    c->oom_halvings++;
+  }
 }
 
 static hipEvent_t take_event(blsv_ctx* c) {
@@ -308,8 +215,9 @@ static int run_lat(blsv_ctx* c, size_t n, LatFn lat, uint64_t* d_bitmap, unsigne
   return BLSV_OK;
 }
 
-// lat_max is clamped to kMaxChunk on every path that sets it; the min keeps the bound local anyway
-static bool use_lat(const blsv_ctx* c, size_t n) { return n > 0 && n <= std::min(c->lat_max, kMaxChunk); }
+// lat_max is clamped to the context's chunk on every path that sets it (the latency kernels write one
+// class byte per item into the chunk-sized class buffer); the min keeps the bound local anyway
+static bool use_lat(const blsv_ctx* c, size_t n) { return n > 0 && n <= std::min(c->lat_max, c->cap); }
 
 struct NoLat {
   void operator()(uint8_t*) const {}
@@ -382,6 +290,62 @@ static int upload_messages(blsv_ctx* c, const uint8_t* msgs, const uint32_t* msg
   HIPCHK(c, hipMemcpyAsync(c->in_len.p, msg_lens, n * 4, hipMemcpyHostToDevice, c->stream));
   // keep the host vectors alive until the copies complete
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return BLSV_OK;
+}
+
+int svc_verify_mixed(blsv_ctx* c, size_t n, const uint8_t* msgs, const uint64_t* off, const uint32_t* lens,
+                     const uint8_t* sigs96, const uint32_t* idx, const uint32_t* d_tab, const uint8_t* d_tab_inf,
+                     uint8_t* cls_out) {
+  if (!n) return BLSV_OK;
+  if (n > kMaxChunk) return fail(c, BLSV_EINVAL, "service batch larger than %zu", kMaxChunk);
+  (void)hipSetDevice(c->device);
+  int rc = ensure_workspace(c, std::min(n, c->chunk));
+  if (rc) return rc;
+  // packed upload: off[n + 1] | lens[n] | idx[n] | sigs[n][96] | message bytes (8-byte aligned parts)
+  const size_t mbytes = off[n];
+  const size_t o_len = (n + 1) * 8, o_idx = o_len + ((n * 4 + 7) & ~size_t(7)),
+               o_sig = o_idx + ((n * 4 + 7) & ~size_t(7)), o_msg = o_sig + n * 96, total = o_msg + mbytes + 8;
+  HIPCHK(c, c->pin.ensure(std::max(total, n + 8)));
+  uint8_t* h = c->pin.as<uint8_t>();
+  memcpy(h, off, (n + 1) * 8);
+  memcpy(h + o_len, lens, n * 4);
+  memcpy(h + o_idx, idx, n * 4);
+  memcpy(h + o_sig, sigs96, n * 96);
+  if (mbytes) memcpy(h + o_msg, msgs, mbytes);
+  HIPCHK(c, c->arena.ensure(total));
+  HIPCHK(c, c->misc.ensure(n + 64));
+  HIPCHK(c, hipMemcpyAsync(c->arena.p, h, total, hipMemcpyHostToDevice, c->stream));
+  uint8_t* d = c->arena.as<uint8_t>();
+  const uint64_t* d_off = reinterpret_cast<const uint64_t*>(d);
+  const uint32_t* d_len = reinterpret_cast<const uint32_t*>(d + o_len);
+  const uint32_t* d_idx = reinterpret_cast<const uint32_t*>(d + o_idx);
+  const uint8_t* d_sig = d + o_sig;
+  const uint8_t* d_msg = d + o_msg;
+  if (use_lat(c, n)) {
+    blsk::launch_lat_messages(d_msg, d_off, d_len, d_sig, 96, 0, n, d_tab, d_tab_inf, d_idx, c->misc.as<uint8_t>(),
+                              nullptr, nullptr, c->stream);
+  } else {
+    const size_t words = (n + 63) / 64;
+    HIPCHK(c, c->bitmap.ensure(words * 8 + 8));
+    HIPCHK(c, c->first_bad.ensure(8));
+    HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
+    const PkSel pk{d_tab, d_tab_inf, d_idx};
+    for (size_t base = 0; base < n; base += c->cap) {
+      const size_t cnt = std::min(c->cap, n - base);
+      rc = run_head(c, d_sig, 96, 0, base, cnt, c->stream, [&]() {
+        blsk::launch_hash_messages(d_msg, d_off + base, d_len + base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(),
+                                   c->HQ.as<uint32_t>(), c->stream);
+      });
+      if (rc) return rc;
+      rc = run_tail(c, d_sig, 96, 0, base, cnt, pk, c->bitmap.as<uint64_t>(), c->first_bad.as<unsigned long long>(),
+                    c->misc.as<uint8_t>(), c->stream);
+      if (rc) return rc;
+    }
+  }
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(h, c->misc.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  memcpy(cls_out, h, n);
   return BLSV_OK;
 }
 
@@ -595,7 +559,6 @@ int blsv_verify_messages(blsv_ctx* c, const uint8_t* pk48, const uint8_t* msgs, 
 // shared by verify_partials / recover: returns per-partial class in cls (host), S staged on device
 // msg_lens == nullptr: every partial signs the same msg[0 .. msg_len); else partial i signs its own
 // message, msgs packed back to back with msg_lens[i] bytes each.
-constexpr size_t kPkTable = 4096;  // member indices with a precomputed PK_i (drand groups are far smaller)
 
 // PK_i = PubPoly.Eval(i) for every member index below min(n, kPkTable) (key/keys.go:239-241; share
 // x = i + 1), built once per group: the partial verifications index this table instead of running
@@ -628,7 +591,7 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
   cls.assign(k, BLSV_REJ_OK);
   index.assign(k, 0);
   if (!c->has_group) return fail(c, BLSV_ENOGROUP, "partials: no group set");
-  if (k > kMaxChunk) return fail(c, BLSV_EINVAL, "partials: too many partials");
+  if (k > c->chunk) return fail(c, BLSV_EINVAL, "partials: more than the context chunk (%zu) in one call", c->chunk);
   for (size_t i = 0; i < k; i++) {
     if (partial_len < 2) {
       cls[i] = BLSV_REJ_SHARE_INDEX;
@@ -643,6 +606,7 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
   if (rc) return rc;
   rc = ensure_workspace(c, k);
   if (rc) return rc;
+  if (k > c->cap) return fail(c, BLSV_EINVAL, "partials: more than the context chunk (%zu) in one call", c->cap);
   // H(msg) once per item slot (all identical); the per-item PubPoly.Eval(index) table
   std::vector<uint32_t> lens(k, (uint32_t)msg_len);
   std::vector<uint8_t> packed;
@@ -900,10 +864,14 @@ int blsv_sign(blsv_ctx* c, const uint8_t* sk32, int32_t index, const uint8_t* ms
   HIPCHK(c, c->sk.ensure(32));
   HIPCHK(c, c->out.ensure(n * stride));
   HIPCHK(c, hipMemcpyAsync(c->sk.p, sk, 32, hipMemcpyHostToDevice, c->stream));
-  blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), n,
-                             c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
-  blsk::launch_sign(c->sk.as<uint32_t>(), index, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), n, c->out.as<uint8_t>(),
-                    stride, c->stream);
+  for (size_t base = 0; base < n; base += c->cap) {  // H staging holds one chunk
+    const size_t cnt = std::min(c->cap, n - base);
+    blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>() + base,
+                               c->in_len.as<uint32_t>() + base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(),
+                               c->HQ.as<uint32_t>(), c->stream);
+    blsk::launch_sign(c->sk.as<uint32_t>(), index, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), cnt,
+                      c->out.as<uint8_t>() + base * stride, stride, c->stream);
+  }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(out, c->out.p, n * stride, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -995,10 +963,18 @@ int blsv_profile_read(blsv_ctx* c, double* ms, uint64_t* launches, uint64_t* ite
   return ST_N;
 }
 
+int blsv_lat_trace_enable(blsv_ctx* c, int on) {
+  if (!c) return BLSV_EINVAL;
+  (void)hipSetDevice(c->device);
+  if (blsk::lat_trace_enable(on, c->stream) != 0) return fail(c, BLSV_EHIP, "lat_trace_enable: symbol copy failed");
+  return BLSV_OK;
+}
+
 int blsv_lat_trace(blsv_ctx* c, uint64_t* ticks, int n, double* ticks_per_us, int clear) {
   if (!c || n < 0 || (n && !ticks)) return BLSV_EINVAL;
   (void)hipSetDevice(c->device);
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // the marks are device-global: wait for every latency launch on the device (any stream, any context)
+  HIPCHK(c, hipDeviceSynchronize());
   int got = 0;
   if (n) {
     got = blsk::lat_trace_read(ticks, n, c->stream);
@@ -1018,8 +994,32 @@ int blsv_lat_trace(blsv_ctx* c, uint64_t* ticks, int n, double* ticks_per_us, in
 size_t blsv_set_lat_max(blsv_ctx* c, size_t lat_max) {
   if (!c) return 0;
   const size_t prev = c->lat_max;
-  c->lat_max = std::min(lat_max, kMaxChunk);  // see lat_max_env: larger batches take the pipeline
+  c->lat_max = std::min(lat_max, c->chunk);  // see lat_max_env: larger batches take the pipeline
   return prev;
+}
+
+// per-context pass size (include/blsverify.h memory contract)
+size_t blsv_set_chunk(blsv_ctx* c, size_t items) {
+  if (!c) return 0;
+  const size_t prev = c->chunk;
+  size_t v = items ? std::min(std::max(items, kMinChunk), kMaxChunk) : chunk_env();
+  v = (v + 63) & ~size_t(63);
+  (void)hipSetDevice(c->device);
+  if (v < c->cap) {  // give the HBM back now: the next call allocates at the new size
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->side);
+    release_workspace(c);
+  }
+  c->chunk = v;
+  c->lat_max = std::min(c->lat_max, v);
+  return prev;
+}
+
+size_t blsv_workspace_bytes(const blsv_ctx* c) {
+  if (!c) return 0;
+  size_t b = 0;
+  for (const DBuf* d : {&c->H, &c->HQ, &c->S, &c->F, &c->FW, &c->LN, &c->h_inf, &c->s_inf, &c->cls}) b += d->sz;
+  return b;
 }
 
 // ------------------------------------------------------------------ testing hooks
@@ -1062,6 +1062,7 @@ int blsv_test_final_exp(blsv_ctx* c, const uint32_t* f, size_t n, uint32_t* out_
   (void)hipSetDevice(c->device);
   int rc = ensure_workspace(c, n);
   if (rc) return rc;
+  if (n > c->cap) return fail(c, BLSV_EINVAL, "test_final_exp: more than the context chunk");
   if (!n) return BLSV_OK;
   DBuf din, dout, dref;
   HIPCHK(c, din.ensure(n * 576));
@@ -1090,6 +1091,7 @@ int blsv_test_hash_to_g2(blsv_ctx* c, const uint8_t* msgs, const uint32_t* msg_l
   (void)hipSetDevice(c->device);
   int rc = ensure_workspace(c, n);
   if (rc) return rc;
+  if (n > c->cap) return fail(c, BLSV_EINVAL, "test_hash_to_g2: more than the context chunk");
   rc = upload_messages(c, msgs, msg_lens, n);
   if (rc) return rc;
   DBuf dout;

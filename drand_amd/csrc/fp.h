@@ -447,10 +447,92 @@ DI void fp2_arg_store(const u24& b) {
   for (int i = 0; i < 24; i++) g_fp2_arg[i * BLS_LANES + l] = b[i];
 }
 
+// Fp2 product with three products per column (Karatsuba inside the column loop) and two reductions:
+//   W  = a0 (b0 + b1)                   shared by both outputs
+//   c0 = W + b1 (32p - a0 - a1)          = a0 b0 - a1 b1 + 32p b1
+//   c1 = W + b0 (a1 + 16p - a0)          = a0 b1 + a1 b0 + 16p b0
+// Column k forms W_k in its own 64-bit register, the second product of each output directly in that
+// output's accumulator, and adds W_k to both (one v_lshl_add_u64 each): 3 x 196 product MADs + 2 x 196
+// reduction MADs against 4 x 196 + 2 x 196 for the two-term dot products. The negations are formed
+// limb-wise against NEG28_32P / NEG28_16P (no borrows: a0, a1 < 8p, the operand contract above
+// fp_mul_u12), so every column sum is non-negative: W < 14 * 2^57, b1 (32p - a0 - a1) < 14 * 2^58,
+// b0 (a1 + 16p - a0) < 14 * 2^57.6, the reduction < 14 * 2^56: < 2^62.6 with the carry. Values (a, b
+// < 8p): c0 < 64p^2 + 256p^2, c1 < 128p^2 + 128p^2, so each result (T + m p) / R < 2p.
+DI void fp2_mont_kara_t(const uint32_t (&x0)[14], const uint32_t (&ys)[14], const uint32_t (&y1)[14],
+                        const uint32_t (&xz)[14], const uint32_t (&y0)[14], const uint32_t (&xy)[14],
+                        uint32_t (&t0)[14], uint32_t (&t1)[14]) {
+  uint32_t m0[14], m1[14];
+  uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    const int lo = k > 13 ? k - 13 : 0, hi = k < 13 ? k : 13;
+    uint64_t w = 0;
+#pragma unroll
+    for (int j = lo; j <= hi; j++) {
+      w += (uint64_t)x0[j] * ys[k - j];
+      c0 += (uint64_t)y1[j] * xz[k - j];
+      c1 += (uint64_t)y0[j] * xy[k - j];
+    }
+    c0 += w;
+    c1 += w;
+    if (k < 14) {
+#pragma unroll
+      for (int j = 0; j < k; j++) {
+        c0 += (uint64_t)m0[j] * P28[k - j];
+        c1 += (uint64_t)m1[j] * P28[k - j];
+      }
+      m0[k] = ((uint32_t)c0 * P_INV28) & M28;
+      m1[k] = ((uint32_t)c1 * P_INV28) & M28;
+      c0 += (uint64_t)m0[k] * P28[0];
+      c1 += (uint64_t)m1[k] * P28[0];
+    } else {
+#pragma unroll
+      for (int j = k - 13; j < 14; j++) {
+        c0 += (uint64_t)m0[j] * P28[k - j];
+        c1 += (uint64_t)m1[j] * P28[k - j];
+      }
+      t0[k - 14] = (uint32_t)c0 & M28;
+      t1[k - 14] = (uint32_t)c1 & M28;
+    }
+    c0 >>= 28;
+    c1 >>= 28;
+  }
+  t0[13] = (uint32_t)c0;
+  t1[13] = (uint32_t)c1;
+}
+
+// BLS_FP2_KARA: the called body (fp2_mul_u24 and the tri.h slot forms); BLS_FP2_KARA_INL: the forms
+// expanded in place (tower.h fp2_mul_inl), whose kernels run call-free at 2 waves/SIMD and feel its
+// larger working set (two reductions in flight instead of one) as spills.
+#ifndef BLS_FP2_KARA
+#define BLS_FP2_KARA 1
+#endif
+#ifndef BLS_FP2_KARA_INL
+#define BLS_FP2_KARA_INL 0
+#endif
+
+DI u24 fp2_mul_body_kara(const u24& a, const u12& b0, const u12& b1) {
+  uint32_t x0[14], x1[14], y0[14], y1[14], ys[14], xz[14], xy[14], t0[14], t1[14];
+  fp_split28(u24_lo(a), x0);
+  fp_split28(u24_hi(a), x1);
+  fp_split28(b0, y0);
+  fp_split28(b1, y1);
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    ys[k] = y0[k] + y1[k];
+    xz[k] = NEG28_32P[k] - x0[k] - x1[k];
+    xy[k] = x1[k] + (NEG28_16P[k] - x0[k]);
+  }
+  fp2_mont_kara_t(x0, ys, y1, xz, y0, xy, t0, t1);
+  return u24_of(fp_join28(t0), fp_join28(t1));
+}
+
 // Fp2 product (a0 + a1 i)(b0 + b1 i) in one body:
 //   c0 = a0 b0 + a1 (16p - b1), c1 = a0 b1 + a1 b0
 // i.e. two reductions instead of three multiplications' worth (counted as the 3 of Karatsuba).
-DI u24 fp2_mul_body(const u24& a, const u12& b0, const u12& b1) {
+template <bool KARA>
+DI u24 fp2_mul_body_t(const u24& a, const u12& b0, const u12& b1) {
+  if (KARA) return fp2_mul_body_kara(a, b0, b1);
   uint32_t x0[14], x1[14], y0[14], y1[14], yn[14];
   fp_split28(u24_lo(a), x0);
   fp_split28(u24_hi(a), x1);
@@ -462,6 +544,7 @@ DI u24 fp2_mul_body(const u24& a, const u12& b0, const u12& b1) {
   const u12 c1 = fp_mont_dot<true>(x0, y1, x1, y0);
   return u24_of(c0, c1);
 }
+DI u24 fp2_mul_body(const u24& a, const u12& b0, const u12& b1) { return fp2_mul_body_t<BLS_FP2_KARA>(a, b0, b1); }
 
 // Fp2 square: c0 = (a0 + a1)(a0 + 16p - a1), c1 = (2 a0) a1, the sums formed limb-wise in radix 2^28
 // after splitting a0 and a1 once (no carry chains: a0 + a1 has limbs < 2^29, a0 + 16p - a1 < 2^29.6

@@ -9,6 +9,7 @@
 
 namespace wv {
 __device__ uint64_t g_lat_trace[LAT_TRACE_N];
+__device__ uint32_t g_lat_trace_on;  // 0 (production) unless blsv_lat_trace_enable turned it on
 static_assert(TEAM_WAVES == WV_WAVES, "one wave of the workgroup per team member");
 }
 
@@ -111,6 +112,14 @@ int lat_trace_clear(hipStream_t st) {
   return hipMemcpyToSymbolAsync(HIP_SYMBOL(wv::g_lat_trace), z, sizeof z, 0, hipMemcpyHostToDevice, st) == hipSuccess
              ? 0
              : -1;
+}
+
+int lat_trace_enable(int on, hipStream_t st) {
+  static const uint32_t v[2] = {0u, 1u};
+  if (hipMemcpyToSymbolAsync(HIP_SYMBOL(wv::g_lat_trace_on), &v[on ? 1 : 0], sizeof(uint32_t), 0,
+                             hipMemcpyHostToDevice, st) != hipSuccess)
+    return -1;
+  return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
 }
 
 void launch_lat_chained(const ChainedSrc& src, size_t base, size_t cnt, const uint32_t* pk_tab, const uint8_t* pk_inf,

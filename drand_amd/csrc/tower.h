@@ -50,7 +50,7 @@ DI fp2 fp2_mul_inl(const fp2& a, const fp2& b) {
   BLS_COUNT_MUL();
   BLS_COUNT_MUL();
   BLS_COUNT_MUL();
-  return fp2_from_u24(fp2_mul_body(fp2_to_u24(a), fp_to_u12(b.c0), fp_to_u12(b.c1)));
+  return fp2_from_u24(fp2_mul_body_t<BLS_FP2_KARA_INL>(fp2_to_u24(a), fp_to_u12(b.c0), fp_to_u12(b.c1)));
 }
 DI fp2 fp2_sqr_inl(const fp2& a) {
   BLS_COUNT_MUL();

@@ -41,16 +41,18 @@
 
 namespace wv {
 
-// Phase trace of the latency kernel (blsv_lat_trace): wave-lane 0 of item 0 (block 0) stamps the
-// device wall clock at the marks of wvteam.h verify_team; a no-op in every other block and on the host.
+// Phase trace of the latency kernel (blsv_lat_trace): while profiling has turned the device-global
+// flag on (blsv_lat_trace_enable), wave-lane 0 of item 0 (block 0) stamps the device wall clock at the
+// marks of wvteam.h verify_team; a no-op in every other block, in production launches and on the host.
 constexpr int LAT_TRACE_N = 16;
 #ifdef WV_HOST
 #define WV_MARK(k) ((void)0)
 #else
 extern __device__ uint64_t g_lat_trace[LAT_TRACE_N];
-#define WV_MARK(k)                                                                     \
-  do {                                                                                 \
-    if (blockIdx.x == 0 && (threadIdx.x & 63u) == 0u) g_lat_trace[(k)] = wall_clock64(); \
+extern __device__ uint32_t g_lat_trace_on;
+#define WV_MARK(k)                                                                                 \
+  do {                                                                                             \
+    if (blockIdx.x == 0 && (threadIdx.x & 63u) == 0u && g_lat_trace_on) g_lat_trace[(k)] = wall_clock64(); \
   } while (0)
 #endif
 

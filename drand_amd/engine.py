@@ -307,9 +307,14 @@ class Engine:
                  "final_exp", "pow1_start", "pow1_end", "xmd_done", "sswu_done", "iso_add_done", "cofactor_done",
                  "sig_sqrt_done", "sig_subgroup_done")
 
+    def lat_trace_enable(self, on=True):
+        """Turn the latency kernel's phase marks on or off (a device-global flag, off by default)."""
+        self._check(self.lib.blsv_lat_trace_enable(self._h, 1 if on else 0))
+
     def lat_trace(self, clear=True):
         """Phase marks (microseconds from the first mark) of item 0 of the last latency-path launch
-        (blsv_lat_trace); marks never stamped are left out."""
+        while marks are enabled (blsv_lat_trace_enable, blsv_lat_trace); marks never stamped are left
+        out."""
         n = len(self.LAT_MARKS)
         t = (ctypes.c_uint64 * n)()
         rate = ctypes.c_double()
@@ -321,8 +326,18 @@ class Engine:
 
     # ------------------------------------------------------------------ testing hooks
     def set_lat_max(self, n):
-        """Batches of at most n items take the latency path (one wave per item); returns the old cutover."""
+        """Batches of at most n items take the latency path (one 8-wave workgroup per item; default
+        1,536, clamped to the chunk); returns the old cutover."""
         return self.lib.blsv_set_lat_max(self._h, int(n))
+
+    def set_chunk(self, items):
+        """Cap the items per pipeline pass (~41.4 KB of HBM staging per item; 0 = the default 2^20);
+        returns the previous chunk (blsv_set_chunk)."""
+        return self.lib.blsv_set_chunk(self._h, int(items))
+
+    def workspace_bytes(self):
+        """HBM bytes of pipeline staging this context holds (blsv_workspace_bytes)."""
+        return self.lib.blsv_workspace_bytes(self._h)
 
     def test_fp_mul(self, a_limbs, b_limbs):
         n = len(a_limbs) // 12
@@ -357,6 +372,65 @@ class Engine:
         self._check(self.lib.blsv_test_hash_to_g2(self._h, _lib.buf(b"".join(bytes(m) for m in msgs)), lens, n, O,
                                                   inf))
         return list(O)[:n * 48], list(inf)[:n]
+
+
+class Service:
+    """Thread-safe front end (blsv_service_*): any number of threads call verify_partial /
+    verify_recovered at once; items that arrive together are verified in one launch. ctypes releases
+    the GIL for the duration of each call, so Python threads block in C side by side."""
+
+    def __init__(self, device: int = 0, gap_us: int = 0, max_wait_us: int = 0, init_torch: bool = True):
+        if init_torch:
+            try:
+                import torch
+            except ImportError:
+                torch = None
+            if torch is not None:
+                torch.cuda.set_device(int(device))
+                torch.zeros(1, device=torch.device("cuda", int(device)))
+        self.lib = _lib.load()
+        h = ctypes.c_void_p()
+        rc = self.lib.blsv_service_create(int(device), int(gap_us), int(max_wait_us), ctypes.byref(h))
+        if rc != 0:
+            raise EngineError(rc, f"blsv_service_create(device={device}) failed")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.blsv_service_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def verify_partial(self, commits, n, msg, partial):
+        """key.Scheme.VerifyPartial(pubPoly, msg, partial): (ok, reject class)."""
+        cb = b"".join(bytes(c) for c in commits)
+        ok, cls = ctypes.c_uint8(), ctypes.c_uint8()
+        p = bytes(partial)
+        rc = self.lib.blsv_service_verify_partial(self._h, _lib.buf(cb), len(commits), int(n), _lib.buf(msg), len(msg),
+                                                  _lib.buf(p), len(p), ctypes.byref(ok), ctypes.byref(cls))
+        if rc != 0:
+            raise EngineError(rc, "blsv_service_verify_partial failed")
+        return bool(ok.value), cls.value
+
+    def verify_recovered(self, pk48, msg, sig96):
+        """key.Scheme.VerifyRecovered(pub, msg, sig): (ok, reject class)."""
+        ok, cls = ctypes.c_uint8(), ctypes.c_uint8()
+        rc = self.lib.blsv_service_verify_recovered(self._h, _lib.buf(pk48), _lib.buf(msg), len(msg), _lib.buf(sig96),
+                                                    ctypes.byref(ok), ctypes.byref(cls))
+        if rc != 0:
+            raise EngineError(rc, "blsv_service_verify_recovered failed")
+        return bool(ok.value), cls.value
+
+    def stats(self):
+        """(launches, items, largest batch) since creation."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self.lib.blsv_service_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
 
 
 def limbs_of(v, n=12):

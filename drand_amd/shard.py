@@ -101,6 +101,11 @@ def combine(first_bad, bitmap_words, count: int, group=None, to_host: bool = Tru
       all-gather of the lengths first (not on the bench path).
     With the gloo backend and a device tensor (two ranks sharing one GPU in the tests) the buffer is
     all-reduced through a host copy.
+    Cost on the RCCL ("nccl") branch -- unmeasured here, run only by the driver's 8-GPU scaling job
+    (this repository's GPU boxes have one GPU; the tests run the gloo branch): a ring all-reduce moves
+    2(N-1)/N of the buffer per rank, about twice what a bitmap all-gather would, i.e. ~22 MB per rank
+    for configs[3]'s 100M rounds at N = 8 (12.5 MB buffer), an estimated ~0.2-0.3 ms over xGMI against
+    ~6 s of verification per 12.5M-round shard.
     Returns (first_bad, bitmap):
       to_host=True : (global first bad round or NONE_U64, list of 64-bit words at global positions)
       to_host=False: (1-element int64 tensor, INT64_MAX = none; int64 words at global bit positions),

@@ -18,8 +18,10 @@
  *  - Bitmaps: bit i (byte i/8, bit i%8, LSB first) = 1 iff item i verified.
  *  - first_bad: the ROUND number (chained/unchained) or the INDEX (message batches) of the first
  *    rejected item, UINT64_MAX when every item verified.
- *  - A context owns one HIP stream and is not thread-safe; use one context per calling thread
- *    (the Go adapter serialises with a mutex or keeps a pool).
+ *  - A context owns one HIP stream and is not thread-safe: one thread calls it at a time. For
+ *    concurrent single-item callers use a blsv_service (thread-safe, coalesces concurrent calls into
+ *    one launch; see the end of this header); for concurrent batch callers one context per thread,
+ *    each with its chunk sized so that all of them fit in HBM (memory contract below).
  *
  * Latency contract (single-item and small callers: client.Get's per-round verify,
  * client/verify.go:185-207; the gossip validator, lp2p/client/validator.go:64; per-packet
@@ -30,8 +32,9 @@
  *    VerifyRecovered 2.3 ms; blsv_aggregate of an n = 64 / t = 33 round (64 VerifyPartial +
  *    Recover + VerifyRecovered) 6.8 ms. Up to 256 items the time stays ~2.5 ms (every item has its
  *    own CU), then grows ~2.35 ms per further 256 items (profiles/r04zk_latency_sweep.json).
- *  - Larger calls run on the BATCH pipeline (one lane per item, staged kernels): ~19 ms floor, then
- *    ~0.5 us per item (about 2 M items/s). Both paths give identical verdicts, reject classes and
+ *  - Larger calls run on the BATCH pipeline (one lane per item, staged kernels): ~16 ms floor
+ *    (profiles/r04zk_latency_sweep.json), then ~0.5 us per item (about 2 M items/s). Both paths give
+ *    identical verdicts, reject classes and
  *    recovered bytes (tests/test_gpu_lat.py runs the same vectors through both).
  *  - The first call on a context also pays allocation and module load (~10-250 ms).
  */
@@ -238,6 +241,63 @@ int blsv_synchronize(blsv_ctx* ctx);
  * are clamped to 2^20. Returns the previous value.
  */
 size_t blsv_set_lat_max(blsv_ctx* ctx, size_t lat_max);
+
+/*
+ * Memory contract. A context allocates its pipeline staging lazily, for min(largest batch, chunk)
+ * items at ~41.4 KB per item (39 KB of it the Miller line staging): a lone verify or a round of
+ * partials takes a few MB, a full 2^20 chunk ~43 GB of the GPU's 288 GB. The chunk defaults to 2^20
+ * (the BLSV_CHUNK environment variable overrides it); a larger batch runs in chunk-sized passes with
+ * identical verdicts. When an allocation fails with out-of-memory the context frees its staging,
+ * halves its chunk (not below 16,384 items) and retries, so contexts or ranks sharing one GPU degrade
+ * to smaller passes instead of failing. blsv_set_chunk caps it explicitly (items, rounded up to a
+ * multiple of 64 and clamped to [16384, 2^20]; 0 = the default) and releases the staging at once when
+ * it shrinks; it also clamps lat_max. Returns the previous chunk.
+ */
+size_t blsv_set_chunk(blsv_ctx* ctx, size_t items);
+/* HBM bytes of pipeline staging the context holds now (0 before its first batch). */
+size_t blsv_workspace_bytes(const blsv_ctx* ctx);
+
+/* ---------------------------------------------------------------- thread-safe service
+ *
+ * Concurrent single-item callers: the reference verifies each arrival in its own goroutine -- one per
+ * partial packet (core/drand_public.go:39 -> chain/beacon/node.go:112,125), one per gossip message
+ * (lp2p/client/validator.go:64), one per client.Get (client/verify.go:185-207). A blsv_service may be
+ * called from any number of threads at once. Each call blocks until its item is verified; the items of
+ * calls that arrive close together are coalesced into ONE launch (the latency path up to lat_max
+ * items, the batch pipeline beyond) by the service's dispatcher thread, and every caller gets its own
+ * verdict. Coalescing window: after the first waiting item the dispatcher keeps gathering while new
+ * items keep arriving within gap_us of the previous one, for at most max_wait_us (0, 0 = the defaults
+ * 150 us and 2000 us; the BLSV_SVC_GAP_US / BLSV_SVC_MAX_WAIT_US environment variables override the
+ * defaults); items that arrive while a launch runs form the next batch. The service owns one context
+ * whose chunk is capped at 65,536 items (~2.7 GB of staging at most).
+ */
+typedef struct blsv_service blsv_service;
+
+int blsv_service_create(int device, uint32_t gap_us, uint32_t max_wait_us, blsv_service** out);
+/* Waits for the items already submitted, then stops the dispatcher. No call may be in flight or follow. */
+void blsv_service_destroy(blsv_service* svc);
+
+/*
+ * key.Scheme.VerifyPartial(pubPoly, msg, partial) (chain/beacon/node.go:112,125): the group is passed
+ * with every call as its t commitments (48 bytes each) and size n, like the reference's per-call
+ * *share.PubPoly; the service keeps the PK_i tables of the groups it has seen (reshare transitions keep
+ * two alive). *ok = 1/0, *reject_class (optional) = BLSV_REJ_*. Returns BLSV_EINVAL for a group whose
+ * commitments do not decode (the call's own error, other callers are unaffected).
+ */
+int blsv_service_verify_partial(blsv_service* svc, const uint8_t* commits48, size_t t, size_t n, const uint8_t* msg,
+                                size_t msg_len, const uint8_t* partial, size_t partial_len, uint8_t* ok,
+                                uint8_t* reject_class);
+
+/*
+ * key.Scheme.VerifyRecovered(pub, msg, sig) (chain/beacon.go:91 via chain.VerifyBeacon; the gossip
+ * validator and client.Get verify one beacon each) against the 48-byte compressed G1 key pk48.
+ * Returns BLSV_EINVAL for a key that does not decode (kilic G1.FromCompressed).
+ */
+int blsv_service_verify_recovered(blsv_service* svc, const uint8_t* pk48, const uint8_t* msg, size_t msg_len,
+                                  const uint8_t* sig96, uint8_t* ok, uint8_t* reject_class);
+
+/* Counters since creation: launches, items verified, the largest batch. Any pointer may be NULL. */
+int blsv_service_stats(blsv_service* svc, uint64_t* launches, uint64_t* items, uint64_t* max_batch);
 
 #ifdef __cplusplus
 }

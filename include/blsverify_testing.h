@@ -42,16 +42,20 @@ int blsv_test_hash_to_g2(blsv_ctx* ctx, const uint8_t* msgs, const uint32_t* msg
  */
 int blsv_profile_enable(blsv_ctx* ctx, int on);
 /*
- * Phase marks of the latency path (k_lat.hip): item 0 of the last latency launch stamps the device
- * wall clock at up to 16 marks of wvteam.h verify_team (0 start, 1 hash done, 2 signature decoded,
- * 3 signature pair's Miller loop done, 4 phase A joined, 5 key pair's Miller loop done, 6 Miller
- * product ready, 7 final exponentiation done, 8/9 first exponentiation by |x| start/end, 10-13 hash:
- * xmd done, both SSWU maps done, isogeny + addition done, cofactor cleared, 14 signature's square
- * root done (before its subgroup check)). Copies n
- * marks (0 = never stamped) into ticks, the clock rate into *ticks_per_us, and zeroes the marks when
- * clear != 0. Returns the number of marks copied.
+ * Phase marks of the latency path (k_lat.hip). Off by default: blsv_lat_trace_enable(ctx, 1) turns
+ * them on for the whole device (one device-global flag; production launches never stamp), 0 off again.
+ * While on, item 0 of each latency launch stamps the device wall clock at up to 16 marks of wvteam.h
+ * verify_team (0 start, 1 hash done, 2 signature decoded, 3 signature pair's Miller loop done, 4 phase
+ * A joined, 5 key pair's Miller loop done, 6 Miller product ready, 7 final exponentiation done, 8/9
+ * first exponentiation by |x| start/end, 10-13 hash: xmd done, both SSWU maps done, isogeny + addition
+ * done, cofactor cleared, 14 signature's square root done (before its subgroup check), 15 signature
+ * subgroup check done). The marks are one device-global array: blsv_lat_trace waits for the whole
+ * device (every stream of every context) before it copies n marks (0 = never stamped) into ticks,
+ * the clock rate into *ticks_per_us, and zeroes the marks when clear != 0. Returns the number of
+ * marks copied. Meant for one profiling process running one latency launch at a time.
  */
 int blsv_lat_trace(blsv_ctx* ctx, uint64_t* ticks, int n, double* ticks_per_us, int clear);
+int blsv_lat_trace_enable(blsv_ctx* ctx, int on);
 int blsv_profile_read(blsv_ctx* ctx, double* ms, uint64_t* launches, uint64_t* items, int nstages);
 
 #ifdef __cplusplus

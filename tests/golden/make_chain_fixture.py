@@ -1,7 +1,8 @@
 """Generate tests/golden/chain2049.bin: one CONTINUOUS 2,049-round chained history (raw 96-byte
 compressed signatures, rounds 1..2049) for the latency-path parity tests at the sizes that path
-serves (tests/test_gpu_lat_scale.py: 1,000 = configs[0], 2,048 = the default cutover, 2,049 = one
-past it). A continuous chain is sequential to sign (sig_i signs Message(i, sig_{i-1})), which is why
+serves (tests/test_gpu_lat_scale.py: 1,000 = configs[0], 1,536 = the default cutover, 1,537 = one
+past it, 2,048 = above it; the tests force each route through set_lat_max, so the cutover a fixture
+was made at does not matter). A continuous chain is sequential to sign (sig_i signs Message(i, sig_{i-1})), which is why
 it is committed instead of generated on the test box.
 
 Recipe: client/test/result/mock/result.go:98-132 with the golden chained key and genesis seed

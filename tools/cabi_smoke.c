@@ -10,16 +10,19 @@
  *      blsv_verify_messages accepts it (and rejects it under another message);
  *   4. the golden n=64/t=33 threshold round: every partial verifies, Recover of a shuffled
  *      33-subset is the group signature, blsv_aggregate_round gives the V1 and V2 group signatures;
- *   5. latency of one lone VerifyRecovered (blsv_verify_messages, n = 1).
+ *   5. latency of one lone VerifyRecovered (blsv_verify_messages, n = 1);
+ *   6. the thread-safe service (blsv_service_*): 64 pthreads each verify ONE golden partial at the
+ *      same moment (one corrupted), every verdict right, the wall time of all 64 against a lone call.
  *
  * Prints one line per check and "cabi_smoke ok" at the end; exit status 0 only if all pass.
  * Build: make -C tools cabi_smoke (gcc, links -lblsverify with an rpath to drand_amd/).
  */
-#define _POSIX_C_SOURCE 199309L
+#define _POSIX_C_SOURCE 200112L
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 #include <time.h>
 
 #include "../include/blsverify.h"
@@ -83,6 +86,24 @@ static int count(const char* key) {
 static void check(int cond, const char* what) {
   printf("%s %s\n", cond ? "PASS" : "FAIL", what);
   if (!cond) failures++;
+}
+
+/* 6. one thread of the service burst: waits at the barrier, verifies its partial */
+typedef struct {
+  blsv_service* svc;
+  const uint8_t *commits, *msg, *partial;
+  size_t t, n, msg_len;
+  pthread_barrier_t* bar;
+  uint8_t ok, cls;
+  int rc;
+} svc_job_t;
+
+static void* svc_worker(void* p) {
+  svc_job_t* j = (svc_job_t*)p;
+  pthread_barrier_wait(j->bar);
+  j->rc = blsv_service_verify_partial(j->svc, j->commits, j->t, j->n, j->msg, j->msg_len, j->partial, 98, &j->ok,
+                                      &j->cls);
+  return NULL;
 }
 
 static double now_ms(void) {
@@ -209,6 +230,56 @@ int main(int argc, char** argv) {
   }
   check(bm[0] & 1, "verify_chained: lone round 1 accepts");
   printf("INFO lone verify latency: %.2f ms\n", best);
+
+  /* 6. the service under 64 concurrent callers */
+  {
+    blsv_service* svc = NULL;
+    RC(blsv_service_create(0, 0, 0, &svc));
+    uint8_t bad[98];
+    memcpy(bad, p1 + 98 * 5, 98);
+    bad[50] ^= 4;
+    uint8_t o = 0, k = 0;
+    RC(blsv_service_verify_partial(svc, commits, (size_t)nc, (size_t)gn, msg1->data, msg1->len, p1, 98, &o, &k));
+    check(o == 1 && k == 0, "service: lone partial accepts (warm-up)");
+    double lone = 1e30;
+    for (int r = 0; r < 5; r++) {
+      double a = now_ms();
+      RC(blsv_service_verify_partial(svc, commits, (size_t)nc, (size_t)gn, msg1->data, msg1->len, p1 + 98, 98, &o,
+                                     &k));
+      double d = now_ms() - a;
+      lone = d < lone ? d : lone;
+    }
+    enum { NT = 64 };
+    svc_job_t jobs[NT];
+    pthread_t th[NT];
+    pthread_barrier_t bar;
+    double burst = 1e30;
+    int right = 1;
+    for (int rep = 0; rep < 3; rep++) {
+      pthread_barrier_init(&bar, NULL, NT + 1);
+      for (int i = 0; i < NT; i++) {
+        jobs[i] = (svc_job_t){svc, commits, msg1->data, i == 5 ? bad : p1 + 98 * (i % np), (size_t)nc, (size_t)gn,
+                              msg1->len, &bar, 0, 0, 0};
+        pthread_create(&th[i], NULL, svc_worker, &jobs[i]);
+      }
+      pthread_barrier_wait(&bar);
+      double a = now_ms();
+      for (int i = 0; i < NT; i++) pthread_join(th[i], NULL);
+      double d = now_ms() - a;
+      burst = d < burst ? d : burst;
+      pthread_barrier_destroy(&bar);
+      for (int i = 0; i < NT; i++)
+        right &= jobs[i].rc == 0 && jobs[i].ok == (i != 5) && jobs[i].cls == (i == 5 ? BLSV_REJ_PAIRING : 0);
+    }
+    uint64_t la = 0, it = 0, mb = 0;
+    RC(blsv_service_stats(svc, &la, &it, &mb));
+    check(right, "service: 64 concurrent VerifyPartial, each verdict right (one corrupted share rejects)");
+    check(burst <= 2.0 * lone, "service: 64 concurrent calls within 2x one lone call");
+    printf("INFO service: lone VerifyPartial %.2f ms, 64 concurrent %.2f ms (best of 3), %llu launches for %llu items,"
+           " largest batch %llu\n",
+           lone, burst, (unsigned long long)la, (unsigned long long)it, (unsigned long long)mb);
+    blsv_service_destroy(svc);
+  }
 
   blsv_destroy(ctx);
   printf("%s (%d failures)\n", failures ? "cabi_smoke FAILED" : "cabi_smoke ok", failures);

@@ -81,9 +81,11 @@ def main():
 
         med, mn = timed(lone_beacon, a.reps)
         out["lone_verify_beacon"] = {"median_ms": med, "min_ms": mn, "stages_ms": stages(eng, lone_beacon)}
+        eng.lat_trace_enable(True)
         eng.lat_trace(clear=True)
         lone_beacon()
         out["lone_verify_beacon"]["phases_us"] = {k: round(v, 1) for k, v in eng.lat_trace().items()}
+        eng.lat_trace_enable(False)
 
         eng.set_group(commits, th["n"])
 

@@ -153,7 +153,7 @@ static int cmd_powfuzz(unsigned long n) {
     x.l[11] &= 0x1fffffffu;
     return x;
   };
-  unsigned long bad_pow = 0, bad_sqr = 0;
+  unsigned long bad_pow = 0, bad_sqr = 0, bad_mul = 0;
   for (unsigned long t = 0; t < n; t++) {
     fp x = rnd2p();
     if (t == 0) x = fp_zero();
@@ -170,9 +170,42 @@ static int cmd_powfuzz(unsigned long n) {
       const fp2 want = {fp_mul(fp_add(red.c0, red.c1), fp_sub(red.c0, red.c1)), fp_dbl(fp_mul(red.c0, red.c1))};
       bad_sqr += !fp2_eq(got, want);
     }
+    // Fp2 product (fp.h: three products per column) on operands of every lazy level up to < 8p,
+    // against the two-term dot-product body and Fp products; the result must also be < 2p
+    auto lvl = [&](int l) {
+      fp v = rnd2p();
+      if (l >= 1) v = fp_add_lazy(v, rnd2p());
+      if (l >= 2) v = fp_add_lazy(v, fp_add_lazy(rnd2p(), rnd2p()));
+      if (l == 3) {  // the largest 12-word value below 8p
+        for (int i = 0; i < 12; i++) v.l[i] = P2_RAW[i];
+        v = fp_add_lazy(fp_add_lazy(v, v), fp_add_lazy(v, v));
+        v.l[0] -= 1;
+      }
+      return v;
+    };
+    for (int l = 0; l < 16; l++) {
+      const fp2 x = {lvl(l & 3), lvl((l >> 2) & 3)}, y = {lvl((l + 1) & 3), lvl((l >> 1) & 3)};
+      const u24 k = fp2_mul_body_kara(fp2_to_u24(x), fp_to_u12(y.c0), fp_to_u12(y.c1));
+      uint32_t x0[14], x1[14], y0[14], y1[14], yn[14];
+      fp_split28(fp_to_u12(x.c0), x0);
+      fp_split28(fp_to_u12(x.c1), x1);
+      fp_split28(fp_to_u12(y.c0), y0);
+      fp_split28(fp_to_u12(y.c1), y1);
+      fp_neg28(y1, yn);
+      const fp2 d = {fp_from_u12(fp_mont_dot<true>(x0, y0, x1, yn)), fp_from_u12(fp_mont_dot<true>(x0, y1, x1, y0))};
+      const fp2 got = fp2_from_u24(k);
+      bool in_range = true;
+      for (const fp* c : {&got.c0, &got.c1}) {
+        unsigned br = 0;
+        for (int i = 0; i < 12; i++) (void)__builtin_subc(c->l[i], P2_RAW[i], br, &br);
+        in_range = in_range && br;
+      }
+      bad_mul += !fp2_eq(got, d) || !in_range;
+    }
   }
-  printf("{\"inputs\": %lu, \"pow_mismatch\": %lu, \"fp2_sqr_mismatch\": %lu}\n", n, bad_pow, bad_sqr);
-  return (bad_pow || bad_sqr) ? 1 : 0;
+  printf("{\"inputs\": %lu, \"pow_mismatch\": %lu, \"fp2_sqr_mismatch\": %lu, \"fp2_mul_mismatch\": %lu}\n", n, bad_pow,
+         bad_sqr, bad_mul);
+  return (bad_pow || bad_sqr || bad_mul) ? 1 : 0;
 }
 
 int main(int argc, char** argv) {

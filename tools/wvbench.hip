@@ -11,6 +11,7 @@
 
 namespace wv {
 __device__ uint64_t g_lat_trace[LAT_TRACE_N];
+__device__ uint32_t g_lat_trace_on;  // wfield.h WV_MARK: off here (no trace in the microbenchmark)
 }
 using namespace wv;
 
