@@ -17,7 +17,7 @@
 
 namespace blsv_detail {
 
-// Beacons per pipeline pass. The staging of one pass is kStagingBytesPerItem per item (~41.4 KB, 39 KB
+// Beacons per pipeline pass. The staging of one pass is kStagingBytesPerItem per item (~42.4 KB, 39 KB
 // of it the Miller line staging): ~43 GB of the 288 GB at the full 2^20 chunk. A context's chunk is
 // capped by blsv_set_chunk / BLSV_CHUNK and halves itself when an allocation fails (ensure_workspace).
 constexpr size_t kMaxChunk = size_t(1) << 20;

@@ -331,7 +331,7 @@ class Engine:
         return self.lib.blsv_set_lat_max(self._h, int(n))
 
     def set_chunk(self, items):
-        """Cap the items per pipeline pass (~41.4 KB of HBM staging per item; 0 = the default 2^20);
+        """Cap the items per pipeline pass (~42.4 KB of HBM staging per item; 0 = the default 2^20);
         returns the previous chunk (blsv_set_chunk)."""
         return self.lib.blsv_set_chunk(self._h, int(items))
 

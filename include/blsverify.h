@@ -244,7 +244,7 @@ size_t blsv_set_lat_max(blsv_ctx* ctx, size_t lat_max);
 
 /*
  * Memory contract. A context allocates its pipeline staging lazily, for min(largest batch, chunk)
- * items at ~41.4 KB per item (39 KB of it the Miller line staging): a lone verify or a round of
+ * items at ~42.4 KB per item (39 KB of it the Miller line staging): a lone verify or a round of
  * partials takes a few MB, a full 2^20 chunk ~43 GB of the GPU's 288 GB. The chunk defaults to 2^20
  * (the BLSV_CHUNK environment variable overrides it); a larger batch runs in chunk-sized passes with
  * identical verdicts. When an allocation fails with out-of-memory the context frees its staging,

@@ -207,4 +207,4 @@ def test_chunk_cap_same_verdicts(engine, golden, C):
     # a corrupted sig_i fails round i and round i + 1 unless i + 1 starts a segment (its prev is a seed)
     want = sorted({i for i in hit} | {i + 1 for i in hit if i + 1 < n and (i + 1) % seg})
     assert bad == want
-    assert 0 < ws <= (1 << 18) * 41500, ws
+    assert 0 < ws <= (1 << 18) * 42500, ws  # ~42.4 KB of staging per item (engine_ctx.h)
