@@ -18,16 +18,131 @@
 #pragma once
 #include "soa.h"
 
+namespace bls {
+
+struct fp4 {
+  fp2 a, b;  // a + b s
+};
+
+// (a + b s)^2 = (a^2 + xi b^2) + 2ab s with SEVEN radix-2^28 product columns and four reductions
+// (a, b < 2p), against ten products for four separate dot products (fp4_sqr_dot below):
+//   Y.a.c0 = A + T - V      A = (a0 + a1)(a0 - a1)   T = (b0 + b1)(b0 - b1)   V = (2 b0) b1
+//   Y.a.c1 = C + T + V      C = (2 a0) a1            (a^2 + xi b^2: xi (x0 + x1 i) = (x0 - x1) + (x0 + x1) i)
+//   Y.b    = a (2b)         Karatsuba columns as fp2_mul_body_kara (three products, two reductions)
+// T and V are formed once per column and added to both outputs. The differences a0 - a1, b0 - b1
+// are SIGNED limbs (|.| < 2^28, products through v_mad_i64_i32), so every column of the Y.a pair
+// stays within a signed 64-bit accumulator: |A_k|, |T_k| < 14 * 2^57, V_k, C_k < 14 * 2^57, the
+// reduction < 14 * 2^56: |column| < 2^62.5. The totals can be negative (A + T - V >= -16 p^2,
+// C + T + V >= -4 p^2), so a result may come out in (-p/128, 0): one conditional + p puts it in
+// [0, 2p). Y.b: a0, a1 < 2p and 2b0, 2b1 < 4p keep fp2_mul_body_kara's bounds (its operands < 8p).
+DI void fp4_sqr_ya_t(const uint32_t (&a0)[14], const uint32_t (&a1)[14], const uint32_t (&b0)[14],
+                     const uint32_t (&b1)[14], uint32_t (&t0)[14], uint32_t (&t1)[14], bool& neg0, bool& neg1) {
+  int32_t am[14], bm[14];
+  uint32_t ap[14], bp[14], a02[14], b02[14];
+#pragma unroll
+  for (int k = 0; k < 14; k++) {
+    ap[k] = a0[k] + a1[k];
+    am[k] = (int32_t)a0[k] - (int32_t)a1[k];
+    bp[k] = b0[k] + b1[k];
+    bm[k] = (int32_t)b0[k] - (int32_t)b1[k];
+    a02[k] = a0[k] << 1;
+    b02[k] = b0[k] << 1;
+  }
+  uint32_t m0[14], m1[14];
+  int64_t c0 = 0, c1 = 0;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {
+    const int lo = k > 13 ? k - 13 : 0, hi = k < 13 ? k : 13;
+    int64_t T = 0;
+    uint64_t V = 0;
+#pragma unroll
+    for (int j = lo; j <= hi; j++) {
+      c0 += (int64_t)(int32_t)ap[j] * (int64_t)am[k - j];
+      c1 += (int64_t)((uint64_t)a02[j] * a1[k - j]);
+      T += (int64_t)(int32_t)bp[j] * (int64_t)bm[k - j];
+      V += (uint64_t)b02[j] * b1[k - j];
+    }
+    c0 += T - (int64_t)V;
+    c1 += T + (int64_t)V;
+    if (k < 14) {
+#pragma unroll
+      for (int j = 0; j < k; j++) {
+        c0 += (int64_t)((uint64_t)m0[j] * P28[k - j]);
+        c1 += (int64_t)((uint64_t)m1[j] * P28[k - j]);
+      }
+      m0[k] = ((uint32_t)c0 * P_INV28) & M28;
+      m1[k] = ((uint32_t)c1 * P_INV28) & M28;
+      c0 += (int64_t)((uint64_t)m0[k] * P28[0]);
+      c1 += (int64_t)((uint64_t)m1[k] * P28[0]);
+    } else {
+#pragma unroll
+      for (int j = k - 13; j < 14; j++) {
+        c0 += (int64_t)((uint64_t)m0[j] * P28[k - j]);
+        c1 += (int64_t)((uint64_t)m1[j] * P28[k - j]);
+      }
+      t0[k - 14] = (uint32_t)c0 & M28;
+      t1[k - 14] = (uint32_t)c1 & M28;
+    }
+    c0 >>= 28;  // arithmetic: the column sums are signed
+    c1 >>= 28;
+  }
+  t0[13] = (uint32_t)c0;
+  t1[13] = (uint32_t)c1;
+  neg0 = c0 < 0;
+  neg1 = c1 < 0;
+}
+
+// 12-word value of limbs t (top limb signed) plus p when neg: [0, 2p) for a value in (-p, p)
+DI u12 fp_join28_fix(const uint32_t (&t)[14], bool neg) {
+  const u12 w = fp_join28(t);
+  const uint32_t msk = neg ? 0xffffffffu : 0u;
+  u12 r;
+  unsigned c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r[i] = __builtin_addc(w[i], P_RAW[i] & msk, c, &c);
+  return r;
+}
+
+DI fp4 fp4_sqr_k7(const fp4& x) {
+  uint32_t a0[14], a1[14], b0[14], b1[14];
+  fp_split28(fp_to_u12(x.a.c0), a0);
+  fp_split28(fp_to_u12(x.a.c1), a1);
+  fp_split28(fp_to_u12(x.b.c0), b0);
+  fp_split28(fp_to_u12(x.b.c1), b1);
+  fp4 y;
+  {
+    uint32_t t0[14], t1[14];
+    bool n0, n1;
+    fp4_sqr_ya_t(a0, a1, b0, b1, t0, t1, n0, n1);
+    y.a.c0 = fp_from_u12(fp_join28_fix(t0, n0));
+    y.a.c1 = fp_from_u12(fp_join28_fix(t1, n1));
+  }
+  BLS_SCHED_FENCE();
+  {
+    uint32_t ys[14], xz[14], xy[14], y0[14], y1[14], t0[14], t1[14];
+#pragma unroll
+    for (int k = 0; k < 14; k++) {  // Y.b = a (2b): y = 2b, limbs < 2^29
+      y0[k] = b0[k] << 1;
+      y1[k] = b1[k] << 1;
+      ys[k] = y0[k] + y1[k];
+      xz[k] = NEG28_32P[k] - a0[k] - a1[k];
+      xy[k] = a1[k] + (NEG28_16P[k] - a0[k]);
+    }
+    fp2_mont_kara_t(a0, ys, y1, xz, y0, xy, t0, t1);
+    y.b.c0 = fp_from_u12(fp_join28(t0));
+    y.b.c1 = fp_from_u12(fp_join28(t1));
+  }
+  return y;
+}
+
+}  // namespace bls
+
 #ifndef BLS_HOST
 namespace bls {
 
 constexpr int TRI_GROUPS = 21;  // beacons per 64-lane wave
 
 // role-dependent additions as one fp_addsub (direction as data) instead of both results + a select
-
-struct fp4 {
-  fp2 a, b;  // a + b s
-};
 
 DI fp4 fp4_add(const fp4& x, const fp4& y) { return {fp2_add(x.a, y.a), fp2_add(x.b, y.b)}; }
 DI fp4 fp4_sub(const fp4& x, const fp4& y) { return {fp2_sub(x.a, y.a), fp2_sub(x.b, y.b)}; }
@@ -155,8 +270,11 @@ DI fp4 tri_conj(const tri_lane& t, const fp4& x) {
 // each lane squares its Fp4 (X = A_j^2); roles 1 and 2 swap their squares; then
 //   role 0, 2: (a, b) <- (3 Y.a - 2 a, 3 Y.b + 2 b)     (role 0: Y = own square, role 2: role 1's)
 //   role 1:    (a, b) <- (3 xi Y.b + 2 a, 3 Y.a - 2 b)  (Y = role 2's square)
+#ifndef BLS_FP4_SQR_K7
+#define BLS_FP4_SQR_K7 1
+#endif
 DI fp4 tri_cyclotomic_sqr(const tri_lane& t, const fp4& x) {
-  const fp4 sq = fp4_sqr_dot(x);
+  const fp4 sq = BLS_FP4_SQR_K7 ? fp4_sqr_k7(x) : fp4_sqr_dot(x);
   const int src = t.role == 1 ? t.next_b : (t.role == 2 ? t.prev_b : (int)(4u * t.lane));
   const fp4 y = xchg_fp4(sq, src);
   const bool r1 = t.role == 1;

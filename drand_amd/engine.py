@@ -417,6 +417,23 @@ class Service:
             raise EngineError(rc, "blsv_service_verify_partial failed")
         return bool(ok.value), cls.value
 
+    def prepare_partial(self, commits, n, msg, partial):
+        """A zero-argument callable doing exactly the ctypes call of verify_partial, its arguments
+        marshalled in advance (so concurrent Python callers hold the GIL only for the call itself)."""
+        cb = _lib.buf(b"".join(bytes(c) for c in commits))
+        mb, pb = _lib.buf(msg), _lib.buf(bytes(partial))
+        t, ml, pl = len(commits), len(msg), len(partial)
+        ok, cls = ctypes.c_uint8(), ctypes.c_uint8()
+        f, h, pok, pcls = self.lib.blsv_service_verify_partial, self._h, ctypes.byref(ok), ctypes.byref(cls)
+
+        def call():
+            rc = f(h, cb, t, n, mb, ml, pb, pl, pok, pcls)
+            if rc != 0:
+                raise EngineError(rc, "blsv_service_verify_partial failed")
+            return bool(ok.value), cls.value
+
+        return call
+
     def verify_recovered(self, pk48, msg, sig96):
         """key.Scheme.VerifyRecovered(pub, msg, sig): (ok, reject class)."""
         ok, cls = ctypes.c_uint8(), ctypes.c_uint8()

@@ -31,14 +31,14 @@ def kernels(co):
     out = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True, text=True, check=True).stdout
     ks, cur = [], {}
     for line in out.splitlines():
-        m = re.match(r"\s*-?\s*\.(\w+):\s+(.*)$", line)
+        m = re.match(r"\s*(-?)\s*\.(\w+):\s+(.*)$", line)
         if not m:
             continue
-        k, v = m.group(1), m.group(2).strip()
+        dash, k, v = m.group(1), m.group(2), m.group(3).strip()
+        if dash and cur:  # a new list entry (each kernel's metadata map starts with "- ")
+            ks.append(cur)
+            cur = {}
         if k in ("agpr_count", "name", "private_segment_fixed_size", "vgpr_count", "sgpr_count"):
-            if k == "name" and "name" in cur:
-                ks.append(cur)
-                cur = {}
             cur[k] = v
     if cur:
         ks.append(cur)

@@ -10,6 +10,7 @@
 
 #include "../drand_amd/csrc/pairing.h"
 #include "../drand_amd/csrc/hash.h"
+#include "../drand_amd/csrc/tri.h"
 
 namespace bls {
 unsigned long long g_fp_mul_count = 0;
@@ -153,7 +154,7 @@ static int cmd_powfuzz(unsigned long n) {
     x.l[11] &= 0x1fffffffu;
     return x;
   };
-  unsigned long bad_pow = 0, bad_sqr = 0, bad_mul = 0;
+  unsigned long bad_pow = 0, bad_sqr = 0, bad_mul = 0, bad_fp4 = 0;
   for (unsigned long t = 0; t < n; t++) {
     fp x = rnd2p();
     if (t == 0) x = fp_zero();
@@ -202,10 +203,29 @@ static int cmd_powfuzz(unsigned long n) {
       }
       bad_mul += !fp2_eq(got, d) || !in_range;
     }
+    // the cyclotomic squaring's Fp4 square (tri.h fp4_sqr_k7: seven product columns, signed Y.a)
+    // against Fp2 squares and products, on reduced inputs including 0, p - 1 and 2p - 1 limbs
+    {
+      fp4 x = {{rnd2p(), rnd2p()}, {rnd2p(), rnd2p()}};
+      if (t % 7 == 1) x.a.c0 = fp_zero();
+      if (t % 7 == 2) for (int i = 0; i < 12; i++) x.b.c1.l[i] = P2_RAW[i] - (i == 0);
+      if (t % 7 == 3) for (int i = 0; i < 12; i++) x.a.c1.l[i] = P2_RAW[i] - (i == 0), x.b.c0.l[i] = 0;
+      if (t % 7 == 4) x.a = fp2_zero();
+      const fp4 y = fp4_sqr_k7(x);
+      const fp2 want_a = fp2_add(fp2_sqr(x.a), fp2_mul_xi(fp2_sqr(x.b)));
+      const fp2 want_b = fp2_dbl(fp2_mul(x.a, x.b));
+      bool in_range = true;
+      for (const fp* c : {&y.a.c0, &y.a.c1, &y.b.c0, &y.b.c1}) {
+        unsigned br = 0;
+        for (int i = 0; i < 12; i++) (void)__builtin_subc(c->l[i], P2_RAW[i], br, &br);
+        in_range = in_range && br;
+      }
+      bad_fp4 += !fp2_eq(y.a, want_a) || !fp2_eq(y.b, want_b) || !in_range;
+    }
   }
-  printf("{\"inputs\": %lu, \"pow_mismatch\": %lu, \"fp2_sqr_mismatch\": %lu, \"fp2_mul_mismatch\": %lu}\n", n, bad_pow,
-         bad_sqr, bad_mul);
-  return (bad_pow || bad_sqr || bad_mul) ? 1 : 0;
+  printf("{\"inputs\": %lu, \"pow_mismatch\": %lu, \"fp2_sqr_mismatch\": %lu, \"fp2_mul_mismatch\": %lu,"
+         " \"fp4_sqr_mismatch\": %lu}\n", n, bad_pow, bad_sqr, bad_mul, bad_fp4);
+  return (bad_pow || bad_sqr || bad_mul || bad_fp4) ? 1 : 0;
 }
 
 int main(int argc, char** argv) {
