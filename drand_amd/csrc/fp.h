@@ -105,12 +105,22 @@ DI fp fp_canon(const fp& a) {
   return r;
 }
 
+// The additive operations below interleave their two carry chains limb by limb (the sum's and the
+// correction's, or the two components' of an Fp2 value): a carry link that reads the previous link's
+// carry needs one wait state on gfx950, which the other chain's link fills -- written chain after
+// chain, the compiler pads every link with s_nop (82 -> 29 pads for two Fp2 additions, tools kt).
 DI fp fp_add(const fp& a, const fp& b) {
-  uint32_t s[12];
-  unsigned c = 0;
+  uint32_t s[12], d[12];
+  unsigned c = 0, br = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) s[i] = __builtin_addc(a.l[i], b.l[i], c, &c);
-  return fp_reduce_2p(s);
+  for (int i = 0; i < 12; i++) {
+    s[i] = __builtin_addc(a.l[i], b.l[i], c, &c);
+    d[i] = __builtin_subc(s[i], P2_RAW[i], br, &br);
+  }
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.l[i] = br ? s[i] : d[i];
+  return r;
 }
 
 DI fp fp_dbl(const fp& a) { return fp_add(a, a); }
@@ -142,16 +152,18 @@ DI fp fp_half(const fp& a) {
 }
 
 // a - b for a, b in [0, 2p): the difference is in (-2p, 2p); 2p is added back on a borrow
+// (a - b and a - b + 2p as two interleaved chains, the borrow of the first picks)
 DI fp fp_sub(const fp& a, const fp& b) {
-  uint32_t d[12];
-  unsigned br = 0;
+  uint32_t d[12], e[12];
+  unsigned br = 0, c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(a.l[i], b.l[i], br, &br);
-  uint32_t m = br ? 0xffffffffu : 0u;
-  unsigned c = 0;
+  for (int i = 0; i < 12; i++) {
+    d[i] = __builtin_subc(a.l[i], b.l[i], br, &br);
+    e[i] = __builtin_addc(d[i], P2_RAW[i], c, &c);
+  }
   fp r;
 #pragma unroll
-  for (int i = 0; i < 12; i++) r.l[i] = __builtin_addc(d[i], P2_RAW[i] & m, c, &c);
+  for (int i = 0; i < 12; i++) r.l[i] = br ? e[i] : d[i];
   return r;
 }
 
@@ -164,12 +176,12 @@ DI fp fp_sub(const fp& a, const fp& b) {
 DI fp fp_addsub(const fp& a, const fp& b, bool sub) {
   const uint32_t m = sub ? 0xffffffffu : 0u;
   uint32_t s[12], d[12];
-  unsigned c1 = sub ? 1u : 0u;
+  unsigned c1 = sub ? 1u : 0u, c2 = sub ? 0u : 1u;
 #pragma unroll
-  for (int i = 0; i < 12; i++) s[i] = __builtin_addc(a.l[i], b.l[i] ^ m, c1, &c1);
-  unsigned c2 = sub ? 0u : 1u;
-#pragma unroll
-  for (int i = 0; i < 12; i++) d[i] = __builtin_addc(s[i], P2_RAW[i] ^ ~m, c2, &c2);
+  for (int i = 0; i < 12; i++) {
+    s[i] = __builtin_addc(a.l[i], b.l[i] ^ m, c1, &c1);
+    d[i] = __builtin_addc(s[i], P2_RAW[i] ^ ~m, c2, &c2);
+  }
   const bool take_d = sub ? (c1 == 0u) : (c2 != 0u);
   fp r;
 #pragma unroll

@@ -272,7 +272,7 @@ int blsv_service_create(int device, uint32_t gap_us, uint32_t max_wait_us, blsv_
     delete s;
     return BLSV_EHIP;
   }
-  const uint32_t gap = gap_us ? gap_us : env_us("BLSV_SVC_GAP_US", 150);
+  const uint32_t gap = gap_us ? gap_us : env_us("BLSV_SVC_GAP_US", 100);
   const uint32_t wait = max_wait_us ? max_wait_us : env_us("BLSV_SVC_MAX_WAIT_US", 2000);
   s->co = std::make_unique<Coalescer<SvcItem>>([s](std::vector<SvcItem*>& b) { s->run(b); }, gap, wait,
                                                kServiceMaxBatch);

@@ -29,11 +29,36 @@ DI fp2 fp2_select(bool c, const fp2& a, const fp2& b) { return {fp_select(c, a.c
 DI fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
 // unreduced sum (< 4p for inputs < 2p; < 8p for two levels): only as a multiplier operand (fp.h
 // operand contract)
-DI fp2 fp2_add_lazy(const fp2& a, const fp2& b) { return {fp_add_lazy(a.c0, b.c0), fp_add_lazy(a.c1, b.c1)}; }
+DI fp2 fp2_add_lazy(const fp2& a, const fp2& b) {  // the two components' chains interleaved (fp.h)
+  fp2 r;
+  unsigned c0 = 0, c1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.l[i] = __builtin_addc(a.c0.l[i], b.c0.l[i], c0, &c0);
+    r.c1.l[i] = __builtin_addc(a.c1.l[i], b.c1.l[i], c1, &c1);
+  }
+  return r;
+}
 DI fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
 DI fp2 fp2_addsub(const fp2& a, const fp2& b, bool sub) { return {fp_addsub(a.c0, b.c0, sub), fp_addsub(a.c1, b.c1, sub)}; }
 DI fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
-DI fp2 fp2_neg(const fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+DI fp2 fp2_neg(const fp2& a) {  // fp_neg per component, the two chains interleaved
+  uint32_t d0[12], d1[12];
+  unsigned b0 = 0, b1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    d0[i] = __builtin_subc(P2_RAW[i], a.c0.l[i], b0, &b0);
+    d1[i] = __builtin_subc(P2_RAW[i], a.c1.l[i], b1, &b1);
+  }
+  const uint32_t m0 = fp_raw_is_zero(a.c0) ? 0u : 0xffffffffu, m1 = fp_raw_is_zero(a.c1) ? 0u : 0xffffffffu;
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.l[i] = d0[i] & m0;
+    r.c1.l[i] = d1[i] & m1;
+  }
+  return r;
+}
 DI fp2 fp2_conj(const fp2& a) { return {a.c0, fp_neg(a.c1)}; }
 
 DI u24 fp2_to_u24(const fp2& a) { return u24_of(fp_to_u12(a.c0), fp_to_u12(a.c1)); }

@@ -267,7 +267,7 @@ size_t blsv_workspace_bytes(const blsv_ctx* ctx);
  * items, the batch pipeline beyond) by the service's dispatcher thread, and every caller gets its own
  * verdict. Coalescing window: after the first waiting item the dispatcher keeps gathering while new
  * items keep arriving within gap_us of the previous one, for at most max_wait_us (0, 0 = the defaults
- * 150 us and 2000 us; the BLSV_SVC_GAP_US / BLSV_SVC_MAX_WAIT_US environment variables override the
+ * 100 us and 2000 us; the BLSV_SVC_GAP_US / BLSV_SVC_MAX_WAIT_US environment variables override the
  * defaults); items that arrive while a launch runs form the next batch. The service owns one context
  * whose chunk is capped at 65,536 items (~2.7 GB of staging at most).
  */
