@@ -26,7 +26,26 @@ DI fp2 fp2_one() { return {fp_one(), fp_zero()}; }
 DI bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) & fp_is_zero(a.c1); }
 DI bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) & fp_eq(a.c1, b.c1); }
 DI fp2 fp2_select(bool c, const fp2& a, const fp2& b) { return {fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
-DI fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+// Fp2 additive operations as four interleaved carry chains (both components' sum and correction):
+// three independent links separate any two dependent ones, so no carry link waits (fp.h fp_add)
+DI fp2 fp2_add(const fp2& a, const fp2& b) {
+  uint32_t s0[12], d0[12], s1[12], d1[12];
+  unsigned c0 = 0, b0 = 0, c1 = 0, b1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    s0[i] = __builtin_addc(a.c0.l[i], b.c0.l[i], c0, &c0);
+    s1[i] = __builtin_addc(a.c1.l[i], b.c1.l[i], c1, &c1);
+    d0[i] = __builtin_subc(s0[i], P2_RAW[i], b0, &b0);
+    d1[i] = __builtin_subc(s1[i], P2_RAW[i], b1, &b1);
+  }
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.l[i] = b0 ? s0[i] : d0[i];
+    r.c1.l[i] = b1 ? s1[i] : d1[i];
+  }
+  return r;
+}
 // unreduced sum (< 4p for inputs < 2p; < 8p for two levels): only as a multiplier operand (fp.h
 // operand contract)
 DI fp2 fp2_add_lazy(const fp2& a, const fp2& b) {  // the two components' chains interleaved (fp.h)
@@ -39,9 +58,45 @@ DI fp2 fp2_add_lazy(const fp2& a, const fp2& b) {  // the two components' chains
   }
   return r;
 }
-DI fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
-DI fp2 fp2_addsub(const fp2& a, const fp2& b, bool sub) { return {fp_addsub(a.c0, b.c0, sub), fp_addsub(a.c1, b.c1, sub)}; }
-DI fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
+DI fp2 fp2_dbl(const fp2& a) { return fp2_add(a, a); }
+DI fp2 fp2_sub(const fp2& a, const fp2& b) {
+  uint32_t d0[12], e0[12], d1[12], e1[12];
+  unsigned b0 = 0, c0 = 0, b1 = 0, c1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    d0[i] = __builtin_subc(a.c0.l[i], b.c0.l[i], b0, &b0);
+    d1[i] = __builtin_subc(a.c1.l[i], b.c1.l[i], b1, &b1);
+    e0[i] = __builtin_addc(d0[i], P2_RAW[i], c0, &c0);
+    e1[i] = __builtin_addc(d1[i], P2_RAW[i], c1, &c1);
+  }
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.l[i] = b0 ? e0[i] : d0[i];
+    r.c1.l[i] = b1 ? e1[i] : d1[i];
+  }
+  return r;
+}
+DI fp2 fp2_addsub(const fp2& a, const fp2& b, bool sub) {  // fp.h fp_addsub on both components, interleaved
+  const uint32_t m = sub ? 0xffffffffu : 0u;
+  uint32_t s0[12], d0[12], s1[12], d1[12];
+  unsigned c0 = sub ? 1u : 0u, e0 = sub ? 0u : 1u, c1 = c0, e1 = e0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    s0[i] = __builtin_addc(a.c0.l[i], b.c0.l[i] ^ m, c0, &c0);
+    s1[i] = __builtin_addc(a.c1.l[i], b.c1.l[i] ^ m, c1, &c1);
+    d0[i] = __builtin_addc(s0[i], P2_RAW[i] ^ ~m, e0, &e0);
+    d1[i] = __builtin_addc(s1[i], P2_RAW[i] ^ ~m, e1, &e1);
+  }
+  const bool t0 = sub ? (c0 == 0u) : (e0 != 0u), t1 = sub ? (c1 == 0u) : (e1 != 0u);
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.l[i] = t0 ? d0[i] : s0[i];
+    r.c1.l[i] = t1 ? d1[i] : s1[i];
+  }
+  return r;
+}
 DI fp2 fp2_neg(const fp2& a) {  // fp_neg per component, the two chains interleaved
   uint32_t d0[12], d1[12];
   unsigned b0 = 0, b1 = 0;
@@ -92,7 +147,24 @@ DI fp2 fp2_mul_fp_inl(const fp2& a, const fp& b) {
 DI fp2 fp2_mul3(const fp2& a) { return {fp_mul3(a.c0), fp_mul3(a.c1)}; }
 
 // multiply by xi = 1 + i: (a0 - a1) + (a0 + a1) i
-DI fp2 fp2_mul_xi(const fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+DI fp2 fp2_mul_xi(const fp2& a) {  // (a0 - a1, a0 + a1): four interleaved chains as fp2_sub / fp2_add
+  uint32_t d[12], e[12], s[12], u[12];
+  unsigned bd = 0, ce = 0, cs = 0, bu = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    d[i] = __builtin_subc(a.c0.l[i], a.c1.l[i], bd, &bd);
+    s[i] = __builtin_addc(a.c0.l[i], a.c1.l[i], cs, &cs);
+    e[i] = __builtin_addc(d[i], P2_RAW[i], ce, &ce);
+    u[i] = __builtin_subc(s[i], P2_RAW[i], bu, &bu);
+  }
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.l[i] = bd ? e[i] : d[i];
+    r.c1.l[i] = bu ? s[i] : u[i];
+  }
+  return r;
+}
 
 DI fp2 fp2_inv(const fp2& a) {
   fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));

@@ -221,6 +221,17 @@ static int cmd_powfuzz(unsigned long n) {
         in_range = in_range && br;
       }
       bad_fp4 += !fp2_eq(y.a, want_a) || !fp2_eq(y.b, want_b) || !in_range;
+      // the interleaved Fp2 additive operations (tower.h) against the per-component fp.h ones
+      const fp2 u = {rnd2p(), rnd2p()}, v = x.b;
+      for (int sub = 0; sub < 2; sub++) {
+        const fp2 g = fp2_addsub(u, v, sub != 0), w = sub ? fp2_sub(u, v) : fp2_add(u, v);
+        const fp2 wr = sub ? fp2{fp_sub(u.c0, v.c0), fp_sub(u.c1, v.c1)} : fp2{fp_add(u.c0, v.c0), fp_add(u.c1, v.c1)};
+        bad_fp4 += !fp2_eq(g, wr) || !fp2_eq(w, wr) || memcmp(&g, &wr, sizeof g) != 0 || memcmp(&w, &wr, sizeof w) != 0;
+      }
+      const fp2 xi = fp2_mul_xi(u), xr = {fp_sub(u.c0, u.c1), fp_add(u.c0, u.c1)};
+      bad_fp4 += memcmp(&xi, &xr, sizeof xi) != 0;
+      const fp2 ng = fp2_neg(u), nr = {fp_neg(u.c0), fp_neg(u.c1)};
+      bad_fp4 += memcmp(&ng, &nr, sizeof ng) != 0;
     }
   }
   printf("{\"inputs\": %lu, \"pow_mismatch\": %lu, \"fp2_sqr_mismatch\": %lu, \"fp2_mul_mismatch\": %lu,"
