@@ -283,6 +283,74 @@ DI g2j g2_madd_inl(const g2j& p, const g2a& q) {
   return out;
 }
 
+// add-2007-bl for the cofactor chains, ordered for the fewest live values: Z3 = 2 (Z1 Z2) H (one more
+// product and one square fewer than (Z1 + Z2)^2 - Z1Z1 - Z2Z2, same value), q's coordinates fetched at
+// their first use (qx(), qy(), qz() re-read them from staging), S1, U1, Z1 Z2 and Z3 parked in LDS
+// between their computation and their uses (three `park` slots), and no exceptional branch: either
+// point at infinity or H == 0 (P == +-Q) sets `exc` and leaves an unspecified result, which the
+// caller replaces by the generic formulas' (k_hash.hip). With both points and the branch's operands
+// live to the end, g2_add_inl spilled ~530 dwords to scratch per addition.
+#ifndef BLS_HOST
+// Per-lane Fp2 slots in LDS (slot k of lane l: six 16-byte words at base[(6k + q) * BLS_LANES + l]),
+// for values that would otherwise stay live in registers across a long stretch of products. The
+// compiler barriers keep the store where it is written and the load from being forwarded from it.
+struct LdsFp2Slots {
+  uint4* base;
+  DI void put(int k, const fp2& v) const {
+    uint4* q = base + 6 * k * BLS_LANES + threadIdx.x;
+#pragma unroll
+    for (int w = 0; w < 3; w++) {
+      q[w * BLS_LANES] = make_uint4(v.c0.l[4 * w], v.c0.l[4 * w + 1], v.c0.l[4 * w + 2], v.c0.l[4 * w + 3]);
+      q[(3 + w) * BLS_LANES] = make_uint4(v.c1.l[4 * w], v.c1.l[4 * w + 1], v.c1.l[4 * w + 2], v.c1.l[4 * w + 3]);
+    }
+    asm volatile("" ::: "memory");
+  }
+  DI fp2 get(int k) const {
+    asm volatile("" ::: "memory");
+    const uint4* q = base + 6 * k * BLS_LANES + threadIdx.x;
+    fp2 v;
+#pragma unroll
+    for (int w = 0; w < 3; w++) {
+      const uint4 a = q[w * BLS_LANES], b = q[(3 + w) * BLS_LANES];
+      v.c0.l[4 * w] = a.x, v.c0.l[4 * w + 1] = a.y, v.c0.l[4 * w + 2] = a.z, v.c0.l[4 * w + 3] = a.w;
+      v.c1.l[4 * w] = b.x, v.c1.l[4 * w + 1] = b.y, v.c1.l[4 * w + 2] = b.z, v.c1.l[4 * w + 3] = b.w;
+    }
+    return v;
+  }
+};
+#else
+// host build (tools/opcount.cpp): the slots are an array of the caller's
+struct LdsFp2Slots {
+  fp2* base;
+  void put(int k, const fp2& v) const { base[k] = v; }
+  fp2 get(int k) const { return base[k]; }
+};
+#endif
+
+template <typename QX, typename QY, typename QZ>
+DI g2j g2_add_inl_exc(const g2j& p, QX qx, QY qy, QZ qz, const LdsFp2Slots& park, bool& exc) {
+  const fp2 Z2 = qz();
+  const fp2 Z2Z2 = fp2_sqr_inl(Z2);
+  park.put(0, fp2_mul_inl(fp2_mul_inl(p.y, Z2), Z2Z2));  // S1
+  park.put(2, fp2_mul_inl(p.x, Z2Z2));                   // U1
+  park.put(1, fp2_mul_inl(p.z, Z2));                     // Z1 Z2
+  exc |= fp2_is_zero(p.z) | fp2_is_zero(Z2);
+  BLS_SCHED_FENCE();
+  const fp2 Z1Z1 = fp2_sqr_inl(p.z);
+  const fp2 S2 = fp2_mul_inl(fp2_mul_inl(qy(), p.z), Z1Z1);
+  BLS_SCHED_FENCE();
+  const fp2 H = fp2_sub(fp2_mul_inl(qx(), Z1Z1), park.get(2));
+  const fp2 r = fp2_dbl(fp2_sub(S2, park.get(0)));
+  exc |= fp2_is_zero(H);
+  park.put(1, fp2_dbl(fp2_mul_inl(park.get(1), H)));  // Z3
+  const fp2 I = fp2_sqr_inl(fp2_dbl(H));
+  const fp2 J = fp2_mul_inl(H, I);
+  const fp2 V = fp2_mul_inl(park.get(2), I);
+  const fp2 X3 = fp2_sub(fp2_sub(fp2_sqr_inl(r), J), fp2_dbl(V));
+  const fp2 Y3 = fp2_sub(fp2_mul_inl(r, fp2_sub(V, X3)), fp2_dbl(fp2_mul_inl(park.get(0), J)));
+  return {X3, Y3, park.get(1)};
+}
+
 // [|x|] P call-free; base() returns P again at each addition (affine for AFF: mixed additions)
 template <bool AFF, typename Base>
 DI g2j g2_mul_x_abs_inl(const g2j& p, Base base) {

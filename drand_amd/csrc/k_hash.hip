@@ -119,19 +119,102 @@ BLS_KERNEL(BLS_WPE_HASH_A) k_hash_messages(const uint8_t* msgs, const uint64_t* 
   hash_a_store<SPLIT>(u0, u1, k, Q, cnt, i);
 }
 
-BLS_KERNEL(BLS_WPE_HASH_B) k_hash_cofactor(uint32_t* Q, size_t cnt) {
+// Phase B. h_eff P = [x]A - A - P + psi^2(2P), A = [x]P + psi(P) (curve.h g2_clear_cofactor_reload),
+// every addition call-free (g2_add_inl_exc) with its second operand fetched from staging one coordinate
+// at a time; only the accumulator lives in registers. Staging: P in slots 0..5 throughout (the
+// exceptional path re-reads it), A and then the partial sum [x]A - A in slots 6..11. A lane whose
+// additions met an exceptional case (a point at infinity, equal or opposite points: never for a hash
+// output in practice) is marked in redo[] and recomputed by k_hash_cofactor_generic with the generic
+// formulas, which handle every case (in a kernel of its own: their called-product frame would size
+// this kernel's scratch at ~10 KB per lane).
+//
+// The sequence runs as a short program of uniform operations (c_cof_prog) over one copy of the
+// doubling and one of the addition: written out, the compiler laid down every addition of both [x]
+// chains separately (200K instructions, ~1.3 MB of code streamed through the instruction cache).
+enum : uint8_t { COF_LOAD, COF_STORE, COF_DBL, COF_ADD, COF_NEG, COF_PSI2, COF_CHECK, COF_END };
+constexpr uint8_t COF_NEGY = 1, COF_PSI = 2;  // COF_ADD flags: q.y negated, q -> psi(q)
+struct CofOp {
+  uint8_t op, arg, flags, pad;  // arg: staging slot (LOAD / STORE / ADD) or doubling count (DBL)
+};
+#define COF_CHAIN(s)                                                                                  \
+  {COF_DBL, 1, 0, 0}, {COF_ADD, s, 0, 0}, {COF_DBL, 2, 0, 0}, {COF_ADD, s, 0, 0}, {COF_DBL, 3, 0, 0}, \
+      {COF_ADD, s, 0, 0}, {COF_DBL, 9, 0, 0}, {COF_ADD, s, 0, 0}, {COF_DBL, 32, 0, 0}, {COF_ADD, s, 0, 0}, \
+      {COF_DBL, 16, 0, 0}  // acc <- [|x|] acc for acc == the point in slot s (bits 62, 60, 57, 48, 16)
+__constant__ CofOp c_cof_prog[] = {
+    {COF_LOAD, 0, 0, 0}, {COF_ADD, 6, 0, 0}, {COF_CHECK, 0, 0, 0}, {COF_STORE, 0, 0, 0},  // P = q0 + q1
+    COF_CHAIN(0), {COF_NEG, 0, 0, 0}, {COF_ADD, 0, COF_PSI, 0}, {COF_STORE, 6, 0, 0},        // A
+    COF_CHAIN(6), {COF_NEG, 0, 0, 0}, {COF_ADD, 6, COF_NEGY, 0}, {COF_STORE, 6, 0, 0},       // R = [x]A - A
+    {COF_LOAD, 0, 0, 0}, {COF_DBL, 1, 0, 0}, {COF_PSI2, 0, 0, 0}, {COF_ADD, 0, COF_NEGY, 0},  // psi^2(2P) - P
+    {COF_ADD, 6, 0, 0}, {COF_STORE, 6, 0, 0}, {COF_END, 0, 0, 0}};                          // + R
+#undef COF_CHAIN
+
+BLS_KERNEL(BLS_WPE_HASH_B) k_hash_cofactor(uint32_t* Q, size_t cnt, uint8_t* redo) {
   size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= cnt) return;
-  store_jac(Q, cnt, i, 0, jac_add(load_jac(Q, cnt, i, 0), load_jac(Q, cnt, i, 6)));
-  auto at = [&](int slot) {
+  auto ld = [&](int slot) {  // re-read at each use, never kept live
     size_t j = i;
-    asm volatile("" : "+v"(j));  // re-read at each use, never kept live across the [x] chains
-    return load_jac(Q, cnt, j, slot);
+    asm volatile("" : "+v"(j));
+    return ld_fp2(Q, cnt, j, slot);
   };
-  // P in slots 0..5; the second chain's base A parks in slots 6..11 (q1 is dead by then)
-  const g2j r = g2_clear_cofactor_inl([&]() { return at(0); }, [&](const g2j& a) { store_jac(Q, cnt, i, 6, a); },
-                                      [&]() { return at(6); });
-  store_jac(Q, cnt, i, 6, r);
+  __shared__ uint4 park_lds[18 * TPB];  // three Fp2 slots per lane (LdsFp2Slots): 18 KB per workgroup, 8 per CU
+  const LdsFp2Slots park = {park_lds};
+  g2j acc = {};
+  bool exc = false;
+#pragma unroll 1
+  for (int pc = 0;; pc++) {
+    const CofOp o = c_cof_prog[pc];
+    if (o.op == COF_END) break;
+    const int s = o.arg;
+    if (o.op == COF_LOAD) {
+      acc = {ld(s), ld(s + 2), ld(s + 4)};
+    } else if (o.op == COF_STORE) {
+      store_jac(Q, cnt, i, s, acc);
+    } else if (o.op == COF_DBL) {
+#pragma unroll 1
+      for (int k = 0; k < s; k++) acc = g2_dbl_inl(acc);
+    } else if (o.op == COF_ADD) {
+      const bool psi = o.flags & COF_PSI, negy = o.flags & COF_NEGY;
+      acc = g2_add_inl_exc(
+          acc,
+          [&]() {
+            const fp2 x = ld(s);
+            return psi ? fp2_mul_inl(fp2_conj(x), fp2_load_const(PSI_KX)) : x;
+          },
+          [&]() {
+            fp2 y = ld(s + 2);
+            if (psi) y = fp2_mul_inl(fp2_conj(y), fp2_load_const(PSI_KY));
+            return negy ? fp2_neg(y) : y;
+          },
+          [&]() {
+            const fp2 z = ld(s + 4);
+            return psi ? fp2_conj(z) : z;
+          },
+          park, exc);
+    } else if (o.op == COF_NEG) {
+      acc.y = fp2_neg(acc.y);
+    } else if (o.op == COF_PSI2) {
+      const fp kx = fp_load_const(PSI2_KX[0]), ky = fp_load_const(PSI2_KY[0]);
+      acc.x = {fp_mul_inl(acc.x.c0, kx), fp_mul_inl(acc.x.c1, kx)};
+      acc.y = {fp_mul_inl(acc.y.c0, ky), fp_mul_inl(acc.y.c1, ky)};
+    } else if (o.op == COF_CHECK) {  // q0 + q1 exceptional: both stay in staging for the generic kernel
+      if (exc) {
+        redo[i] = 2;
+        return;
+      }
+    }
+  }
+  redo[i] = exc;
+}
+
+// Phase B's exceptional lanes, or every lane when `all`: h_eff P by the generic formulas. redo[i] = 2:
+// q0 + q1 met an exceptional case and both are still in slots 0..11; otherwise P is in slots 0..5.
+BLS_KERNEL(BLS_WPE_HASH_B) k_hash_cofactor_generic(uint32_t* Q, size_t cnt, const uint8_t* redo, int all) {
+  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= cnt) return;
+  const uint8_t rd = redo[i];
+  if (!(all || rd)) return;
+  if (rd == 2) store_jac(Q, cnt, i, 0, jac_add(load_jac(Q, cnt, i, 0), load_jac(Q, cnt, i, 6)));
+  store_jac(Q, cnt, i, 6, g2_clear_cofactor_reload([&]() { return load_jac(Q, cnt, i, 0); }));
 }
 
 BLS_KERNEL(BLS_WPE_HASH_C) k_hash_affine(const uint32_t* Q, size_t cnt, uint32_t* H, uint8_t* h_inf) {
@@ -141,8 +224,12 @@ BLS_KERNEL(BLS_WPE_HASH_C) k_hash_affine(const uint32_t* Q, size_t cnt, uint32_t
 }
 
 // ------------------------------------------------------------------ launchers
+// nonzero: every lane takes the generic cofactor clearing (blsv_test_cofactor_generic)
+int g_cofactor_generic_all = 0;
 static void launch_hash_bc(uint32_t* Q, size_t cnt, uint32_t* H, uint8_t* h_inf, hipStream_t st) {
-  hipLaunchKernelGGL(k_hash_cofactor, dim3(grid_for(cnt)), dim3(TPB), 0, st, Q, cnt);
+  hipLaunchKernelGGL(k_hash_cofactor, dim3(grid_for(cnt)), dim3(TPB), 0, st, Q, cnt, h_inf);
+  hipLaunchKernelGGL(k_hash_cofactor_generic, dim3(grid_for(cnt)), dim3(TPB), 0, st, Q, cnt, h_inf,
+                     g_cofactor_generic_all);
   hipLaunchKernelGGL(k_hash_affine, dim3(grid_for(cnt)), dim3(TPB), 0, st, Q, cnt, H, h_inf);
 }
 

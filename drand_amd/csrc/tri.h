@@ -142,6 +142,10 @@ namespace bls {
 
 constexpr int TRI_GROUPS = 21;  // beacons per 64-lane wave
 
+// per-lane LDS columns of the staged product operands (see "low register pressure products" below)
+constexpr int TRI_ARG_WORDS = 72;
+static __shared__ __attribute__((aligned(16))) uint32_t g_tri_arg[TRI_ARG_WORDS * BLS_LANES];
+
 // role-dependent additions as one fp_addsub (direction as data) instead of both results + a select
 
 DI fp4 fp4_add(const fp4& x, const fp4& y) { return {fp2_add(x.a, y.a), fp2_add(x.b, y.b)}; }
@@ -273,10 +277,53 @@ DI fp4 tri_conj(const tri_lane& t, const fp4& x) {
 #ifndef BLS_FP4_SQR_K7
 #define BLS_FP4_SQR_K7 1
 #endif
-DI fp4 tri_cyclotomic_sqr(const tri_lane& t, const fp4& x) {
-  const fp4 sq = BLS_FP4_SQR_K7 ? fp4_sqr_k7(x) : fp4_sqr_dot(x);
+#ifndef BLS_CSQR_PARK
+#define BLS_CSQR_PARK 1
+#endif
+// x parked in this lane's first 48 words of g_tri_arg (the staging slots 0 and 1, free between the
+// products) as 12 16-byte columns: the square's limb arrays then have the register file to themselves
+// (with x held across the square, the K7 body spilled 24 dwords per square to scratch: 18 KB of HBM
+// reads per beacon per fexp launch).
+DI void tri_park4(const fp4& x) {
+  uint4* q = reinterpret_cast<uint4*>(g_tri_arg) + threadIdx.x;
+  const fp2* h[2] = {&x.a, &x.b};
+#pragma unroll
+  for (int s = 0; s < 2; s++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      q[(6 * s + k) * BLS_LANES] = make_uint4(h[s]->c0.l[4 * k], h[s]->c0.l[4 * k + 1], h[s]->c0.l[4 * k + 2], h[s]->c0.l[4 * k + 3]);
+      q[(6 * s + 3 + k) * BLS_LANES] = make_uint4(h[s]->c1.l[4 * k], h[s]->c1.l[4 * k + 1], h[s]->c1.l[4 * k + 2], h[s]->c1.l[4 * k + 3]);
+    }
+}
+DI fp4 tri_unpark4() {
+  const uint4* q = reinterpret_cast<const uint4*>(g_tri_arg) + threadIdx.x;
+  fp4 x;
+  fp2* h[2] = {&x.a, &x.b};
+#pragma unroll
+  for (int s = 0; s < 2; s++)
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const uint4 u = q[(6 * s + k) * BLS_LANES], v = q[(6 * s + 3 + k) * BLS_LANES];
+      h[s]->c0.l[4 * k] = u.x, h[s]->c0.l[4 * k + 1] = u.y, h[s]->c0.l[4 * k + 2] = u.z, h[s]->c0.l[4 * k + 3] = u.w;
+      h[s]->c1.l[4 * k] = v.x, h[s]->c1.l[4 * k + 1] = v.y, h[s]->c1.l[4 * k + 2] = v.z, h[s]->c1.l[4 * k + 3] = v.w;
+    }
+  return x;
+}
+
+DI fp4 tri_cyclotomic_sqr(const tri_lane& t, const fp4& x_in) {
+#if BLS_CSQR_PARK
+  tri_park4(x_in);
+  asm volatile("" ::: "memory");  // the park is neither sunk below the square nor forwarded past it
+#endif
+  const fp4 sq = BLS_FP4_SQR_K7 ? fp4_sqr_k7(x_in) : fp4_sqr_dot(x_in);
   const int src = t.role == 1 ? t.next_b : (t.role == 2 ? t.prev_b : (int)(4u * t.lane));
   const fp4 y = xchg_fp4(sq, src);
+#if BLS_CSQR_PARK
+  asm volatile("" ::: "memory");
+  const fp4 x = tri_unpark4();
+#else
+  const fp4& x = x_in;
+#endif
   const bool r1 = t.role == 1;
   const fp2 u = fp2_select(r1, fp2_mul_xi(y.b), y.a);
   const fp2 v = fp2_select(r1, y.a, y.b);
@@ -324,8 +371,6 @@ DI fp4 tri_sqr(const tri_lane& t, const fp4& a) {
 // 72-word column (3 Fp2 slots). A staged Fp4 y sits there as (y.a, y.b, y.a + y.b), and an Fp4
 // product x y keeps only x and its partial products in VGPRs across the three calls. 72 words x 64
 // lanes = 18 KB per one-wave workgroup: 8 workgroups (2 waves/SIMD) fit the CU's 160 KB.
-constexpr int TRI_ARG_WORDS = 72;
-static __shared__ uint32_t g_tri_arg[TRI_ARG_WORDS * BLS_LANES];
 
 DI void tri_arg_put(int slot, const fp2& v) {
   const unsigned l = threadIdx.x;

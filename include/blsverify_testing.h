@@ -34,6 +34,13 @@ int blsv_test_hash_to_g2(blsv_ctx* ctx, const uint8_t* msgs, const uint32_t* msg
                          uint8_t* inf);
 
 /*
+ * on != 0: every hash's cofactor clearing takes the generic path (k_hash.hip k_hash_cofactor_generic,
+ * the formulas with every exceptional case) instead of only the lanes the call-free chains flag; 0
+ * restores production. One process-global switch (all contexts), for the cross-check of both paths.
+ */
+int blsv_test_cofactor_generic(blsv_ctx* ctx, int on);
+
+/*
  * Stage timing for bench.py's roofline: when enabled, every stage launch (0 hash, 1 decompress,
  * 2 miller, 3 final_exp, 4 finish, 5 lat = a whole batch on the latency path) is bracketed by HIP
  * events on its launch stream. blsv_profile_read waits for the recorded events, writes per-stage

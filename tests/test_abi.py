@@ -121,6 +121,17 @@ def test_host_sqrt_window_and_fp2_sqr_fuzz(opcount_bin):
     out = json.loads(r.stdout)
     assert out["pow_mismatch"] == 0 and out["fp2_sqr_mismatch"] == 0, out
 
+
+def test_host_cofactor_addition_flags_exceptions(opcount_bin):
+    """The cofactor chains' branch-free addition (curve.h g2_add_inl_exc) equals jac_add on distinct
+    points given in different Jacobian representations, and raises its exceptional flag for P + P,
+    P + (-P) and a point at infinity on either side (k_hash.hip then recomputes such lanes with the
+    generic formulas) -- the device source compiled for the host."""
+    r = subprocess.run([opcount_bin, "addfuzz", "2000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert json.loads(r.stdout)["add_mismatch"] == 0
+
+
 def _split_top(args):
     out, depth, cur = [], 0, ""
     for ch in args:

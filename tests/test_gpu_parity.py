@@ -58,6 +58,25 @@ def test_hash_to_g2_both_phase_a_forms(engine, golden):
     assert not any(inf_big) and not any(inf_small)
 
 
+def test_hash_cofactor_generic_path(engine, golden):
+    """Phase B of hash-to-G2 runs the cofactor clearing as call-free chains whose additions flag the
+    exceptional cases (a point at infinity, P == +-Q) instead of branching on them; flagged lanes are
+    recomputed by a second kernel with the generic formulas. Forcing every lane through the generic
+    kernel must give the same points (and the golden ones)."""
+    vecs = golden["hash_to_g2"]
+    msgs = [bytes.fromhex(v["msg"]) for v in vecs] + [b"cofactor %d" % i for i in range(3000)]
+    fast, inf_fast = engine.test_hash_to_g2(msgs)
+    engine.test_cofactor_generic(True)
+    try:
+        slow, inf_slow = engine.test_hash_to_g2(msgs)
+    finally:
+        engine.test_cofactor_generic(False)
+    assert fast == slow and inf_fast == inf_slow
+    for i, v in enumerate(vecs):
+        want = [int(v["x"][0], 16), int(v["x"][1], 16), int(v["y"][0], 16), int(v["y"][1], 16)]
+        assert [from_limbs(slow[48 * i + 12 * s:48 * i + 12 * s + 12]) for s in range(4)] == want
+
+
 def test_pairing_golden(engine, golden):
     """Engine reduced pairing = e(P, Q)^3 (hard part uses 3*(p^4-p^2+1)/r)."""
     for v in golden["pairing"]:

@@ -239,10 +239,58 @@ static int cmd_powfuzz(unsigned long n) {
   return (bad_pow || bad_sqr || bad_mul || bad_fp4) ? 1 : 0;
 }
 
+// The cofactor chains' addition (curve.h g2_add_inl_exc: no exceptional branch, a flag instead)
+// against jac_add on curve points from the SSWU map, each also in a second Jacobian representation
+// (X z^2, Y z^3, Z z): for distinct points the sums agree projectively and the flag stays clear; for
+// P + P, P + (-P) and a point at infinity on either side the flag is set. Prints the mismatch count.
+static int cmd_addfuzz(unsigned long n) {
+  using namespace bls;
+  unsigned long long s = 0x5851f42d4c957f2dull;
+  auto next = [&]() {
+    s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+    return (uint32_t)(s >> 11);
+  };
+  auto rnd = [&]() {
+    fp x;
+    for (int i = 0; i < 12; i++) x.l[i] = next();
+    x.l[11] &= 0x0fffffffu;
+    return fp_to_mont(x);
+  };
+  auto point = [&]() { return hash_field_to_q1(fp2{rnd(), rnd()}); };
+  auto rescale = [&](const g2j& p) {
+    const fp2 z = {rnd(), rnd()}, z2 = fp2_sqr(z);
+    return g2j{fp2_mul(p.x, z2), fp2_mul(p.y, fp2_mul(z2, z)), fp2_mul(p.z, z)};
+  };
+  fp2 slots[3];
+  const LdsFp2Slots park = {slots};
+  unsigned long bad = 0;
+  auto add = [&](const g2j& p, const g2j& q, bool& exc) {
+    exc = false;
+    return g2_add_inl_exc(p, [&]() { return q.x; }, [&]() { return q.y; }, [&]() { return q.z; }, park, exc);
+  };
+  for (unsigned long t = 0; t < n; t++) {
+    const g2j p = point(), q = point(), q2 = rescale(q), p2 = rescale(p);
+    bool exc;
+    const g2j r = add(p, q2, exc);
+    bad += exc || !jac_eq(r, jac_add(p, q));
+    (void)add(p, p2, exc);
+    bad += !exc;
+    (void)add(p, jac_neg(p2), exc);
+    bad += !exc;
+    (void)add(jac_infinity<fp2>(), q, exc);
+    bad += !exc;
+    (void)add(p, jac_infinity<fp2>(), exc);
+    bad += !exc;
+  }
+  printf("{\"inputs\": %lu, \"add_mismatch\": %lu}\n", n, bad);
+  return bad != 0;
+}
+
 int main(int argc, char** argv) {
   if (argc == 3 && !strcmp(argv[1], "hash")) return cmd_hash(argv[2]);
   if (argc == 3 && !strcmp(argv[1], "powfuzz")) return cmd_powfuzz(strtoul(argv[2], nullptr, 10));
   if (argc == 3 && !strcmp(argv[1], "invfuzz")) return cmd_invfuzz(strtoul(argv[2], nullptr, 10));
+  if (argc == 3 && !strcmp(argv[1], "addfuzz")) return cmd_addfuzz(strtoul(argv[2], nullptr, 10));
   if (argc != 5) {
     fprintf(stderr, "usage: %s pk48hex round prevhex|- sig96hex   (prev '-' = unchained V2)\n       %s hash msghex\n",
             argv[0], argv[0]);
