@@ -883,8 +883,8 @@ DI u12 fp_inv_bingcd_raw(u12 yin, bool& converged) {
       f1 = F1;
       g1 = G1;
       A >>= 1;
-      f1 <<= 1;
-      g1 <<= 1;
+      f1 = (int64_t)((uint64_t)f1 << 1);  // 2 f1 (a signed left shift is undefined for f1 < 0 in C++17)
+      g1 = (int64_t)((uint64_t)g1 << 1);
     }
     uint32_t X[14], Y[14];
     u12 av, bv;

@@ -41,7 +41,7 @@ WVI F fp2_from_be512(const uint32_t (&w0)[16], const uint32_t (&w1)[16]) {
   auto limb = [&](uint32_t base) {
     const V lo = lds_ld(lds, h * 16u + base + sel(wi < 8u, wi, vsplat(0)));
     const V hi = lds_ld(lds, h * 16u + base + sel(wi < 7u, wi + 1u, vsplat(0)));
-    const V v = ((lo >> sh) | sel((sh == 0u) | (wi >= 7u), vsplat(0), hi << (32u - sh))) & M25;
+    const V v = ((lo >> sh) | sel((sh == 0u) | (wi >= 7u), vsplat(0), hi << ((32u - sh) & 31u))) & M25;  // (sh == 0: discarded)
     return sel(live, v, vsplat(0));
   };
   const V hv = limb(0), lv = limb(8);

@@ -21,7 +21,7 @@ WVI F fp2_from392(const uint32_t* S, size_t stride, size_t k, int slot) {
   const V f = (uint32_t)slot + h;
   auto word = [&](V w) { return gld(base, (f * 12u + sel(w < 12u, w, vsplat(11))) * (uint32_t)stride); };
   const V lo = word(wi), hi = word(sel(wi < 11u, wi + 1u, vsplat(11)));
-  const V v = ((lo >> sh) | sel((sh == 0u) | (wi >= 11u), vsplat(0), hi << (32u - sh))) & M25;
+  const V v = ((lo >> sh) | sel((sh == 0u) | (wi >= 11u), vsplat(0), hi << ((32u - sh) & 31u))) & M25;  // (sh == 0: discarded)
   return mulp(mkF(sel((l & 16u) == 0u, v, vsplat(0)), 2.0), cst(WC_C408_DUP));
 }
 

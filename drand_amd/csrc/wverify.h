@@ -15,7 +15,7 @@ WVI F g1_coord(const uint32_t* w12) {
   const V l = lane_id(), k = l & 15u;
   const V bit = k * 25u, wi = bit >> 5, sh = bit & 31u;
   const V lo = gld(w12, sel(wi < 12u, wi, vsplat(11))), hi = gld(w12, sel(wi < 11u, wi + 1u, vsplat(11)));
-  const V v = ((lo >> sh) | sel((sh == 0u) | (wi >= 11u), vsplat(0), hi << (32u - sh))) & M25;
+  const V v = ((lo >> sh) | sel((sh == 0u) | (wi >= 11u), vsplat(0), hi << ((32u - sh) & 31u))) & M25;  // (sh == 0: discarded)
   const V limbs = sel((l & 16u) == 0u, v, vsplat(0));
   return mulp(mkF(limbs, 2.0), cst(WC_C408_DUP));  // x 2^392 -> x 2^400
 }

@@ -12,13 +12,15 @@ import pytest
 from oracle import bls12381 as O
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BIN = os.path.join(ROOT, "tools", "wvtest")
+# WVTEST_TARGET=wvtest-asan runs the module on the ASan+UBSan build (tests/test_sanitize.py)
+TARGET = os.environ.get("WVTEST_TARGET", "wvtest")
+BIN = os.path.join(ROOT, "tools", TARGET)
 P = O.P
 
 
 @pytest.fixture(scope="module")
 def wvtest():
-    subprocess.run(["make", "-C", os.path.join(ROOT, "tools"), "wvtest"], check=True, capture_output=True)
+    subprocess.run(["make", "-C", os.path.join(ROOT, "tools"), TARGET], check=True, capture_output=True)
     return BIN
 
 
