@@ -12,6 +12,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of bench.py with BLSV_SERIAL_STAGES=1
 #   pmc              PMC passes: FETCH_SIZE, WRITE_SIZE, two SQ/GRBM sets (tools/pmc_sq.py)
 #   cabi             tools/cabi_smoke (latency contract from plain C)
+#   pmccal           FETCH_SIZE / WRITE_SIZE of tools/pmccal (known bytes in the engine's SoA patterns)
 #   wvbench          tools/wvbench (per-operation latency of the latency engine's primitives)
 #   intrate          tools/intrate (peak v_mad_u64_u32 rate) and its SQ/GRBM counters (clock of the peak)
 #   lat              tools/latency_bench.py (lone verify, fused round)
@@ -66,6 +67,11 @@ for step in "$@"; do
       timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE \
         --output-format csv -d "$O/pmc_intrate" -o run -- tools/intrate > "$O/pmc_intrate.log" 2>&1 &&
       python3 tools/pmc_sq.py "$O/pmc_intrate.json" "$O/pmc_intrate/run_counter_collection.csv" > /dev/null || rc=23 ;;
+    pmccal)
+      timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmccal_fetch" -o run -- tools/pmccal \
+        > "$O/pmccal_fetch.log" 2>&1 &&
+      timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmccal_write" -o run -- tools/pmccal \
+        > "$O/pmccal_write.log" 2>&1 || rc=24 ;;
     cabi) timeout -k 10 120 tools/cabi_smoke > "$O/cabi_smoke.txt" 2>&1 || rc=20 ;;
     wvbench) timeout -k 10 120 tools/wvbench > "$O/wvbench.json" 2>&1 || rc=25 ;;
     lat) timeout -k 10 300 python -u tools/latency_bench.py --reps 10 --out "$O/latency.json" > "$O/latency.log" 2>&1 || rc=21 ;;

@@ -1,8 +1,16 @@
 """Per-stage HBM traffic per beacon from rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; each in its
 own run), corrected as /opt/skills/guides/MI355X_MICROARCH.md "HBM [CDNA4]" prescribes: FETCH_SIZE
 is in KiB and reports 1/2 of the bytes of coalesced streaming reads on gfx950 (doubled here);
-WRITE_SIZE (KiB) is taken as is. Our accesses are dword-per-lane coalesced (256 B per wave
-instruction), a width the guide lists as uncalibrated -- ratios between kernels are reliable.
+WRITE_SIZE (KiB) is taken as is. Our accesses are dword-per-lane, a width the guide lists as
+uncalibrated, so tools/pmccal.hip measured them on a known 576 bytes per item (profiles/r05k_pmccal.json):
+  one lane per item (256 contiguous bytes per wave instruction): FETCH_SIZE = 288 B/item -> x2 exact,
+                                                                 WRITE_SIZE exact;
+  three lanes per item (tri.h, 21 items = 84 bytes per wave instruction): FETCH_SIZE = 713 B/item
+                                                                 -> x0.808, WRITE_SIZE x0.900.
+"bytes_per_beacon" keeps the guide's x2 for every kernel (comparable with earlier rounds);
+"calibrated_bytes_per_beacon" applies the 3-lane factors to the 3-lane kernels (k_fexp_tri,
+k_miller_f_tri), whose staging reads are that pattern (their park and scratch reads are
+one-lane-per-word, so the calibrated figure is a lower estimate for them and the x2 one an upper).
 
 usage: python tools/pmc_traffic.py <fetch_run_counter_collection.csv> <write_...csv> <beacons> [out.json]
 """
@@ -23,14 +31,24 @@ def stage_of(name):
     return None
 
 
-def totals(path, counter):
+TRI_READ, TRI_WRITE = 576.0 / 713.16, 12.0 / 13.33  # tools/pmccal.hip, profiles/r05k_pmccal.json
+
+
+def is_tri(name):
+    return "_tri" in name.split("(")[0]
+
+
+def totals(path, counter, tri_factor=None):
     out = defaultdict(float)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
         st = stage_of(r["Kernel_Name"])
         if st:
-            out[st] += float(r["Counter_Value"]) * 1024.0
+            v = float(r["Counter_Value"]) * 1024.0
+            if tri_factor is not None:
+                v *= tri_factor[1] if is_tri(r["Kernel_Name"]) else tri_factor[0]
+            out[st] += v
     return out
 
 
@@ -44,6 +62,12 @@ def main():
     for st in sorted(set(fetch) | set(write)):
         rd, wr = 2 * fetch.get(st, 0.0) / n, write.get(st, 0.0) / n
         res["bytes_per_beacon"][st] = {"read": round(rd, 1), "write": round(wr, 1), "total": round(rd + wr, 1)}
+    cf = totals(sys.argv[1], "FETCH_SIZE", (2.0, TRI_READ))
+    cw = totals(sys.argv[2], "WRITE_SIZE", (1.0, TRI_WRITE))
+    res["calibrated_bytes_per_beacon"] = {}
+    for st in sorted(set(cf) | set(cw)):
+        rd, wr = cf.get(st, 0.0) / n, cw.get(st, 0.0) / n
+        res["calibrated_bytes_per_beacon"][st] = {"read": round(rd, 1), "write": round(wr, 1), "total": round(rd + wr, 1)}
     txt = json.dumps(res, indent=1)
     if len(sys.argv) > 4:
         open(sys.argv[4], "w").write(txt + "\n")
