@@ -963,9 +963,9 @@ int blsv_profile_read(blsv_ctx* c, double* ms, uint64_t* launches, uint64_t* ite
   return ST_N;
 }
 
-int blsv_test_cofactor_generic(blsv_ctx* c, int on) {
+int blsv_test_generic_chains(blsv_ctx* c, int on) {
   if (!c) return BLSV_EINVAL;
-  blsk::g_cofactor_generic_all = on != 0;
+  blsk::g_generic_chains_all = on != 0;
   return BLSV_OK;
 }
 

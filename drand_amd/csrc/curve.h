@@ -351,6 +351,31 @@ DI g2j g2_add_inl_exc(const g2j& p, QX qx, QY qy, QZ qz, const LdsFp2Slots& park
   return {X3, Y3, park.get(1)};
 }
 
+// madd-2007-bl for the subgroup check's chain in the same low-pressure form as g2_add_inl_exc: q
+// affine, fetched per coordinate (qx(), qy()), Z3 = 2 Z1 H (a product in place of a square and two
+// subtractions), Y1 and Z3 parked in LDS slots 0 and 1 and X1 in slot 2 between their computation and
+// their last use; an exceptional case (p at infinity or H == 0: p == +-q) sets `exc` and leaves an
+// unspecified result.
+template <typename QX, typename QY>
+DI g2j g2_madd_inl_exc(const g2j& p, QX qx, QY qy, const LdsFp2Slots& park, bool& exc) {
+  park.put(0, p.y);
+  park.put(2, p.x);
+  const fp2 Z1Z1 = fp2_sqr_inl(p.z);
+  const fp2 S2 = fp2_mul_inl(fp2_mul_inl(qy(), p.z), Z1Z1);
+  BLS_SCHED_FENCE();
+  const fp2 H = fp2_sub(fp2_mul_inl(qx(), Z1Z1), park.get(2));
+  exc |= fp2_is_zero(p.z) | fp2_is_zero(H);
+  park.put(1, fp2_dbl(fp2_mul_inl(p.z, H)));  // Z3
+  const fp2 r = fp2_dbl(fp2_sub(S2, park.get(0)));
+  BLS_SCHED_FENCE();
+  const fp2 I = fp2_dbl(fp2_dbl(fp2_sqr_inl(H)));
+  const fp2 J = fp2_mul_inl(H, I);
+  const fp2 V = fp2_mul_inl(park.get(2), I);
+  const fp2 X3 = fp2_sub(fp2_sub(fp2_sqr_inl(r), J), fp2_dbl(V));
+  const fp2 Y3 = fp2_sub(fp2_mul_inl(r, fp2_sub(V, X3)), fp2_dbl(fp2_mul_inl(park.get(0), J)));
+  return {X3, Y3, park.get(1)};
+}
+
 // [|x|] P call-free; base() returns P again at each addition (affine for AFF: mixed additions)
 template <bool AFF, typename Base>
 DI g2j g2_mul_x_abs_inl(const g2j& p, Base base) {

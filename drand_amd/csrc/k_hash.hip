@@ -1,5 +1,9 @@
 // Stage 1: drand message derivation + RFC 9380 hash-to-G2, one lane per beacon, in three kernels.
 // chain.Message / MessageV2 (chain/beacon.go:103-114) -> KyberG2.Hash [ext].
+// The in-place Fp2 products of this unit's G2 chains use the Karatsuba body (tower.h
+// fp2_mul_inl): their live state leaves room for its extra operand arrays here, unlike the Miller
+// lines kernel (same-box A/B, profiles/r05_ab.json r05l: hash + decompression 100.7 -> 98.6 ms).
+#define BLS_FP2_KARA_INL 1
 #include "kcommon.h"
 
 namespace blsk {
@@ -224,12 +228,12 @@ BLS_KERNEL(BLS_WPE_HASH_C) k_hash_affine(const uint32_t* Q, size_t cnt, uint32_t
 }
 
 // ------------------------------------------------------------------ launchers
-// nonzero: every lane takes the generic cofactor clearing (blsv_test_cofactor_generic)
-int g_cofactor_generic_all = 0;
+// nonzero: every lane takes the generic cofactor clearing and subgroup check (blsv_test_generic_chains)
+int g_generic_chains_all = 0;
 static void launch_hash_bc(uint32_t* Q, size_t cnt, uint32_t* H, uint8_t* h_inf, hipStream_t st) {
   hipLaunchKernelGGL(k_hash_cofactor, dim3(grid_for(cnt)), dim3(TPB), 0, st, Q, cnt, h_inf);
   hipLaunchKernelGGL(k_hash_cofactor_generic, dim3(grid_for(cnt)), dim3(TPB), 0, st, Q, cnt, h_inf,
-                     g_cofactor_generic_all);
+                     g_generic_chains_all);
   hipLaunchKernelGGL(k_hash_affine, dim3(grid_for(cnt)), dim3(TPB), 0, st, Q, cnt, H, h_inf);
 }
 

@@ -69,7 +69,7 @@ void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap
 int lat_trace_read(uint64_t* out, int n, hipStream_t st);  // phase marks of item 0 (wteam.h WV_MARK)
 int lat_trace_clear(hipStream_t st);
 int lat_trace_enable(int on, hipStream_t st);  // the device-global flag WV_MARK tests (off by default)
-extern int g_cofactor_generic_all;  // k_hash.hip: every lane through k_hash_cofactor_generic (test hook)
+extern int g_generic_chains_all;  // k_hash.hip: every lane through the generic cofactor / subgroup kernels (test hook)
 // and, for the messages form with S != nullptr, the decoded sigma (H/S staging layout, stride cnt)
 void launch_lat_chained(const ChainedSrc& src, size_t base, size_t cnt, const uint32_t* pk_tab, const uint8_t* pk_inf,
                         uint8_t* cls, hipStream_t st);

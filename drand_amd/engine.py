@@ -373,10 +373,11 @@ class Engine:
                                                   inf))
         return list(O)[:n * 48], list(inf)[:n]
 
-    def test_cofactor_generic(self, on=True):
-        """Every hash's cofactor clearing through the generic formulas (k_hash_cofactor_generic)
-        instead of only the lanes the call-free chains flag; process-global, for the parity tests."""
-        self._check(self.lib.blsv_test_cofactor_generic(self._h, 1 if on else 0))
+    def test_generic_chains(self, on=True):
+        """Every hash's cofactor clearing and every signature's subgroup check through the generic
+        formulas (k_hash_cofactor_generic, k_subgroup_g2_generic) instead of only the lanes the
+        call-free chains flag; process-global, for the parity tests."""
+        self._check(self.lib.blsv_test_generic_chains(self._h, 1 if on else 0))
 
 
 class Service:

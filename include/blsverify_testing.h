@@ -34,11 +34,12 @@ int blsv_test_hash_to_g2(blsv_ctx* ctx, const uint8_t* msgs, const uint32_t* msg
                          uint8_t* inf);
 
 /*
- * on != 0: every hash's cofactor clearing takes the generic path (k_hash.hip k_hash_cofactor_generic,
- * the formulas with every exceptional case) instead of only the lanes the call-free chains flag; 0
- * restores production. One process-global switch (all contexts), for the cross-check of both paths.
+ * on != 0: every hash's cofactor clearing and every decoded signature's subgroup check take the
+ * generic path (k_hash.hip k_hash_cofactor_generic, k_decomp.hip k_subgroup_g2_generic: the formulas
+ * with every exceptional case) instead of only the lanes the call-free chains flag; 0 restores
+ * production. One process-global switch (all contexts), for the cross-check of both paths.
  */
-int blsv_test_cofactor_generic(blsv_ctx* ctx, int on);
+int blsv_test_generic_chains(blsv_ctx* ctx, int on);
 
 /*
  * Stage timing for bench.py's roofline: when enabled, every stage launch (0 hash, 1 decompress,

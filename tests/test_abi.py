@@ -123,7 +123,8 @@ def test_host_sqrt_window_and_fp2_sqr_fuzz(opcount_bin):
 
 
 def test_host_cofactor_addition_flags_exceptions(opcount_bin):
-    """The cofactor chains' branch-free addition (curve.h g2_add_inl_exc) equals jac_add on distinct
+    """The cofactor chains' branch-free addition (curve.h g2_add_inl_exc) and the subgroup check's mixed
+    addition (g2_madd_inl_exc) equal jac_add on distinct
     points given in different Jacobian representations, and raises its exceptional flag for P + P,
     P + (-P) and a point at infinity on either side (k_hash.hip then recomputes such lanes with the
     generic formulas) -- the device source compiled for the host."""

@@ -66,15 +66,62 @@ def test_hash_cofactor_generic_path(engine, golden):
     vecs = golden["hash_to_g2"]
     msgs = [bytes.fromhex(v["msg"]) for v in vecs] + [b"cofactor %d" % i for i in range(3000)]
     fast, inf_fast = engine.test_hash_to_g2(msgs)
-    engine.test_cofactor_generic(True)
+    engine.test_generic_chains(True)
     try:
         slow, inf_slow = engine.test_hash_to_g2(msgs)
     finally:
-        engine.test_cofactor_generic(False)
+        engine.test_generic_chains(False)
     assert fast == slow and inf_fast == inf_slow
     for i, v in enumerate(vecs):
         want = [int(v["x"][0], 16), int(v["x"][1], 16), int(v["y"][0], 16), int(v["y"][1], 16)]
         assert [from_limbs(slow[48 * i + 12 * s:48 * i + 12 * s + 12]) for s in range(4)] == want
+
+
+def _small_order_points(q, seed):
+    """All nonzero multiples of a point of order q (13 or 23: both divide the G2 cofactor twice) on
+    the twist E'(Fp2), built with the Python oracle: on the curve, outside G2."""
+    h2 = 0x5d543a95414e7f1091d50792876a202cd91de4547085abaa68a205b2e5a7ddfa628f1cb4d9e82ef21537e293a6691ae1616ec6e786f0c70cf1c38e31c7238e5
+    rng = random.Random(seed)
+    while True:
+        x = (rng.randrange(O.P), rng.randrange(O.P))
+        rhs = O.f2_add(O.f2_mul(O.f2_sqr(x), x), O.B2)
+        if not O.f2_is_square(rhs):
+            continue
+        qp = O.g2_mul((x, O.f2_sqrt(rhs)), h2 * O.R // (q * q))
+        if qp is None:
+            continue
+        base = O.g2_mul(qp, q) or qp
+        assert O.g2_mul(base, q) is None
+        pts, acc = [], None
+        for _ in range(q - 1):
+            acc = O.g2_add(acc, base)
+            pts.append(acc)
+        return pts
+
+
+def test_subgroup_check_small_order_points_both_paths(engine, golden):
+    """Signatures that decode to points of order 13 or 23 (every nonzero multiple): the signature's
+    psi subgroup check must reject them all (REJ_NOT_IN_SUBGROUP) on the batch path, where the
+    call-free chain meets its exceptional cases (the running point equal to +-P or at infinity) and
+    hands those lanes to k_subgroup_g2_generic; forcing every lane through the generic kernel, and
+    the latency path, give the same classes. The golden KAT signature stays valid throughout."""
+    kat = golden["kat"]
+    sigs = [O.g2_compress(pt) for q, seed in ((13, 7), (23, 8)) for pt in _small_order_points(q, seed)]
+    sigs.append(bytes.fromhex(kat["sig"]))
+    msgs = [bytes.fromhex(kat["msg"])] * len(sigs)
+    engine.set_public_key(bytes.fromhex(kat["pk"]))
+    want = [O.REJ_NOT_IN_SUBGROUP] * (len(sigs) - 1) + [0]
+    old = engine.set_lat_max(0)
+    try:
+        assert engine.verify_messages(msgs, sigs).reject_class == want
+        engine.test_generic_chains(True)
+        try:
+            assert engine.verify_messages(msgs, sigs).reject_class == want
+        finally:
+            engine.test_generic_chains(False)
+    finally:
+        engine.set_lat_max(old)
+    assert engine.verify_messages(msgs, sigs).reject_class == want
 
 
 def test_pairing_golden(engine, golden):

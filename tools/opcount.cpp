@@ -239,8 +239,8 @@ static int cmd_powfuzz(unsigned long n) {
   return (bad_pow || bad_sqr || bad_mul || bad_fp4) ? 1 : 0;
 }
 
-// The cofactor chains' addition (curve.h g2_add_inl_exc: no exceptional branch, a flag instead)
-// against jac_add on curve points from the SSWU map, each also in a second Jacobian representation
+// The cofactor chains' addition (curve.h g2_add_inl_exc: no exceptional branch, a flag instead) and
+// the subgroup check's mixed addition (g2_madd_inl_exc) against jac_add on curve points from the SSWU map, each also in a second Jacobian representation
 // (X z^2, Y z^3, Z z): for distinct points the sums agree projectively and the flag stays clear; for
 // P + P, P + (-P) and a point at infinity on either side the flag is set. Prints the mismatch count.
 static int cmd_addfuzz(unsigned long n) {
@@ -268,9 +268,23 @@ static int cmd_addfuzz(unsigned long n) {
     exc = false;
     return g2_add_inl_exc(p, [&]() { return q.x; }, [&]() { return q.y; }, [&]() { return q.z; }, park, exc);
   };
+  auto madd = [&](const g2j& p, const g2a& q, bool& exc) {
+    exc = false;
+    return g2_madd_inl_exc(p, [&]() { return q.x; }, [&]() { return q.y; }, park, exc);
+  };
   for (unsigned long t = 0; t < n; t++) {
     const g2j p = point(), q = point(), q2 = rescale(q), p2 = rescale(p);
     bool exc;
+    // mixed addition (the subgroup check's): q affine
+    const g2a qa = g2_to_aff(q), pa = g2_to_aff(p);
+    const g2j m = madd(p2, qa, exc);
+    bad += exc || !jac_eq(m, jac_add(p, q));
+    (void)madd(p2, pa, exc);
+    bad += !exc;
+    (void)madd(p2, g2a{pa.x, fp2_neg(pa.y)}, exc);
+    bad += !exc;
+    (void)madd(jac_infinity<fp2>(), qa, exc);
+    bad += !exc;
     const g2j r = add(p, q2, exc);
     bad += exc || !jac_eq(r, jac_add(p, q));
     (void)add(p, p2, exc);
