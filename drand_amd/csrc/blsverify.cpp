@@ -37,7 +37,7 @@ int ensure_workspace(blsv_ctx* c, size_t cnt) {
     need(c->F, want * blsk::F_WORDS * 4);
     need(c->FW, 3 * want * blsk::F_WORDS * 4);
     // LN doubles as the final exponentiation's park
-    need(c->LN, std::max(std::min(want, kLineSub) * blsk::MILLER_LINE_WORDS, blsk::FEXP_STAGE_WORDS(want)) * 4);
+    need(c->LN, std::max(std::min(want, kLineSub) * blsk::MILLER_LINE_WORDS, blsk::FEXP_PARK_WORDS(want)) * 4);
     need(c->h_inf, want);
     need(c->s_inf, want);
     need(c->cls, want);

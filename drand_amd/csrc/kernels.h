@@ -58,12 +58,6 @@ constexpr size_t TRI_PARK_WORDS(size_t items) { return 48 * 64 * ((items + 20) /
 // exponentiated values (SoA, cnt * F_WORDS words)
 // park: FEXP_PARK_WORDS(cnt) words of scratch for the 3-lane products' parked partial results
 constexpr size_t FEXP_PARK_WORDS(size_t items) { return TRI_PARK_WORDS(items); }
-// the whole final-exponentiation staging inside LN: the park, six kept powers (Fp12 SoA slots of the
-// compressed squaring chains, k_fexp.hip) and one fallback flag byte per item
-constexpr size_t FEXP_KEPT = 6;
-constexpr size_t FEXP_STAGE_WORDS(size_t items) {
-  return FEXP_PARK_WORDS(items) + FEXP_KEPT * F_WORDS * items + (items + 3) / 4;
-}
 void launch_final_exp(uint32_t* F, uint32_t* W, size_t cnt, uint8_t* cls, hipStream_t st, uint32_t* park,
                       uint32_t* out = nullptr);
 // bitmap bit (base+i) = (cls[i] == 0); bitmap must cover whole 64-bit words;

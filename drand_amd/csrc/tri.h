@@ -135,24 +135,6 @@ DI fp4 fp4_sqr_k7(const fp4& x) {
   return y;
 }
 
-// Karabina's compressed cyclotomic squaring in this basis. For f = A0 + A1 w + A2 w^2 in the
-// cyclotomic subgroup, the Granger-Scott square's new A1 depends only on A2's square and the new A2
-// only on A1's (tri_cyclotomic_sqr, roles 1 and 2), so (A1, A2) can be squared on its own and A0
-// recovered afterwards. With conj(f) = f^(p^6) = Ā0 - Ā1 w + Ā2 w^2 (Ā = a - b s), the w^2 and w^1
-// coefficients of f conj(f) = 1 are linear in A0 = a0 + b0 s:
-//   2 (a0 a2 - xi b0 b2) = a1^2 - xi b1^2 = R1          2 (a0 b1 - a1 b0) = -(a2^2 - xi b2^2) = -R2
-// so with D = 2 (a1 a2 - xi b1 b2) (csq_den):  a0 = (a1 R1 + xi b2 R2) / D,  b0 = (a2 R2 + b1 R1) / D
-// (csq_num). D = 0 (e.g. f = 1) has no such solution: the callers fall back to full squarings.
-DI fp2 csq_den(const fp4& A1, const fp4& A2) {
-  return fp2_dbl(fp2_sub(fp2_mul(A1.a, A2.a), fp2_mul_xi(fp2_mul(A1.b, A2.b))));
-}
-DI void csq_num(const fp4& A1, const fp4& A2, fp2& na, fp2& nb) {
-  const fp2 R1 = fp2_sub(fp2_sqr(A1.a), fp2_mul_xi(fp2_sqr(A1.b)));
-  const fp2 R2 = fp2_sub(fp2_sqr(A2.a), fp2_mul_xi(fp2_sqr(A2.b)));
-  na = fp2_add(fp2_mul(A1.a, R1), fp2_mul_xi(fp2_mul(A2.b, R2)));
-  nb = fp2_add(fp2_mul(A2.a, R2), fp2_mul(A1.b, R1));
-}
-
 }  // namespace bls
 
 #ifndef BLS_HOST

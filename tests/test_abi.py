@@ -133,15 +133,6 @@ def test_host_cofactor_addition_flags_exceptions(opcount_bin):
     assert json.loads(r.stdout)["add_mismatch"] == 0
 
 
-def test_host_compressed_cyclotomic_squaring(opcount_bin):
-    """Karabina's compressed squaring in the thirds basis (tri.h: A1, A2 squared alone, A0 recovered
-    by csq_den / csq_num, the formulas derived from f conj(f) = 1) equals fp12_cyclotomic_sqr after 1..12
-    squarings of random cyclotomic elements -- the device source compiled for the host."""
-    r = subprocess.run([opcount_bin, "csqfuzz", "200"], capture_output=True, text=True)
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert json.loads(r.stdout)["csq_mismatch"] == 0
-
-
 def _split_top(args):
     out, depth, cur = [], 0, ""
     for ch in args:

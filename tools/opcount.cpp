@@ -300,55 +300,11 @@ static int cmd_addfuzz(unsigned long n) {
   return bad != 0;
 }
 
-// Compressed cyclotomic squaring (tri.h): (A1, A2) squared alone, A0 recovered by csq_den / csq_num,
-// against fp12_cyclotomic_sqr on random elements of the cyclotomic subgroup (fexp_easy of random
-// Fp12), after 1..n squarings. Prints the mismatch count.
-static int cmd_csqfuzz(unsigned long n) {
-  using namespace bls;
-  unsigned long long s = 0x853c49e6748fea9bull;
-  auto next = [&]() {
-    s ^= s << 13, s ^= s >> 7, s ^= s << 17;
-    return (uint32_t)(s >> 11);
-  };
-  auto rnd = [&]() {
-    fp x;
-    for (int i = 0; i < 12; i++) x.l[i] = next();
-    x.l[11] &= 0x0fffffffu;
-    return x;
-  };
-  auto rnd2 = [&]() { return fp2{rnd(), rnd()}; };
-  unsigned long bad = 0;
-  for (unsigned long t = 0; t < n; t++) {
-    fp12 f;
-    f.c0 = {rnd2(), rnd2(), rnd2()};
-    f.c1 = {rnd2(), rnd2(), rnd2()};
-    fp12 y = fexp_easy(f);
-    fp4 A1 = {y.c1.c0, y.c0.c2}, A2 = {y.c0.c1, y.c1.c2};
-    for (int k = 0; k < 12; k++) {
-      const fp4 Y1 = fp4_sqr_k7(A1), Y2 = fp4_sqr_k7(A2);
-      const fp4 N1 = {fp2_add(fp2_dbl(fp2_add(fp2_mul_xi(Y2.b), A1.a)), fp2_mul_xi(Y2.b)),
-                      fp2_add(fp2_dbl(fp2_sub(Y2.a, A1.b)), Y2.a)};
-      const fp4 N2 = {fp2_add(fp2_dbl(fp2_sub(Y1.a, A2.a)), Y1.a), fp2_add(fp2_dbl(fp2_add(Y1.b, A2.b)), Y1.b)};
-      A1 = N1, A2 = N2;
-      y = fp12_cyclotomic_sqr(y);
-      fp2 na, nb;
-      csq_num(A1, A2, na, nb);
-      const fp2 di = fp2_inv(csq_den(A1, A2));
-      const fp2 a0 = fp2_mul(na, di), b0 = fp2_mul(nb, di);
-      bad += !fp2_eq(A1.a, y.c1.c0) || !fp2_eq(A1.b, y.c0.c2) || !fp2_eq(A2.a, y.c0.c1) || !fp2_eq(A2.b, y.c1.c2) ||
-             !fp2_eq(a0, y.c0.c0) || !fp2_eq(b0, y.c1.c1);
-    }
-  }
-  printf("{\"inputs\": %lu, \"csq_mismatch\": %lu}\n", n, bad);
-  return bad != 0;
-}
-
 int main(int argc, char** argv) {
   if (argc == 3 && !strcmp(argv[1], "hash")) return cmd_hash(argv[2]);
   if (argc == 3 && !strcmp(argv[1], "powfuzz")) return cmd_powfuzz(strtoul(argv[2], nullptr, 10));
   if (argc == 3 && !strcmp(argv[1], "invfuzz")) return cmd_invfuzz(strtoul(argv[2], nullptr, 10));
   if (argc == 3 && !strcmp(argv[1], "addfuzz")) return cmd_addfuzz(strtoul(argv[2], nullptr, 10));
-  if (argc == 3 && !strcmp(argv[1], "csqfuzz")) return cmd_csqfuzz(strtoul(argv[2], nullptr, 10));
   if (argc != 5) {
     fprintf(stderr, "usage: %s pk48hex round prevhex|- sig96hex   (prev '-' = unchained V2)\n       %s hash msghex\n",
             argv[0], argv[0]);
