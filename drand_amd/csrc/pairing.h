@@ -80,14 +80,14 @@ DI void miller_dbl_step_ts(const TS& t, Put put, XP xp, YP yp) {
   BLS_SCHED_FENCE();
   put(2, fp2_neg(fp2_mul_fp_inl(H, yp())));
   BLS_SCHED_FENCE();
-  t.set(2, fp2_mul_inl(B, H));  // Z3 (Z has had its last use)
+  t.set(2, fp2_mul_inl_k<0>(B, H));  // Z3 (Z has had its last use)
   BLS_SCHED_FENCE();
   const fp2 E = fp2_mul_3b(C);
   const fp2 F = fp2_mul3(E);
   const fp2 G = fp2_half(fp2_add(B, F));
   put(0, fp2_sub(E, B));
   const fp2 BF = fp2_sub(B, F);
-  const fp2 A = fp2_half(fp2_mul_inl(t.get(0), t.get(1)));
+  const fp2 A = fp2_half(fp2_mul_inl_k<1>(t.get(0), t.get(1)));
   BLS_SCHED_FENCE();
   put(1, fp2_mul_fp_inl(fp2_mul3(fp2_sqr_inl(t.get(0))), xp()));
   BLS_SCHED_FENCE();

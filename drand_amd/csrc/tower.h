@@ -126,12 +126,21 @@ DI fp2 fp2_mul(const fp2& a, const fp2& b) {
 }
 DI fp2 fp2_sqr(const fp2& a) { return fp2_from_u24(fp2_sqr_u24(fp2_to_u24(a))); }
 // in-place expansions (no call): for call-free kernels whose register budget must stay small
-DI fp2 fp2_mul_inl(const fp2& a, const fp2& b) {
+template <bool KARA>
+DI fp2 fp2_mul_inl_t(const fp2& a, const fp2& b) {
   BLS_COUNT_MUL();
   BLS_COUNT_MUL();
   BLS_COUNT_MUL();
-  return fp2_from_u24(fp2_mul_body_t<BLS_FP2_KARA_INL>(fp2_to_u24(a), fp_to_u12(b.c0), fp_to_u12(b.c1)));
+  return fp2_from_u24(fp2_mul_body_t<KARA>(fp2_to_u24(a), fp_to_u12(b.c0), fp_to_u12(b.c1)));
 }
+DI fp2 fp2_mul_inl(const fp2& a, const fp2& b) { return fp2_mul_inl_t<BLS_FP2_KARA_INL>(a, b); }
+// the Karatsuba body at the Miller doubling step's call sites whose live state leaves room for it:
+// BLS_LINES_KARA bit 0 = Z3 = B H, bit 1 = A = X Y / 2 (pairing.h miller_dbl_step_ts)
+#ifndef BLS_LINES_KARA
+#define BLS_LINES_KARA 3
+#endif
+template <int SITE>
+DI fp2 fp2_mul_inl_k(const fp2& a, const fp2& b) { return fp2_mul_inl_t<((BLS_LINES_KARA >> SITE) & 1) != 0>(a, b); }
 DI fp2 fp2_sqr_inl(const fp2& a) {
   BLS_COUNT_MUL();
   BLS_COUNT_MUL();
