@@ -232,34 +232,7 @@ DI bool g2_in_subgroup(const g2j& p) {
 // A called Fp2 product makes everything live across it sit in the ~112 callee-saved VGPRs; the
 // chain's point, its base point and a step's temporaries do not fit, so a called addition spills
 // (7 KB/lane at 2 waves/SIMD for the subgroup check) and the chains ran at 1 wave/SIMD. Here the
-// additions are expanded in place too, with the base point re-read from staging at each of its 5
-// uses; only the exceptional cases (P == +-Q, a point at infinity) take a rarely executed branch
-// through the called formulas. Same results as jac_add / jac_add_aff.
-// add-2007-bl (as jac_add)
-DI g2j g2_add_inl(const g2j& p, const g2j& q) {
-  const fp2 Z1Z1 = fp2_sqr_inl(p.z);
-  const fp2 Z2Z2 = fp2_sqr_inl(q.z);
-  const fp2 U1 = fp2_mul_inl(p.x, Z2Z2);
-  const fp2 U2 = fp2_mul_inl(q.x, Z1Z1);
-  const fp2 S1 = fp2_mul_inl(fp2_mul_inl(p.y, q.z), Z2Z2);
-  const fp2 S2 = fp2_mul_inl(fp2_mul_inl(q.y, p.z), Z1Z1);
-  const fp2 H = fp2_sub(U2, U1);
-  const fp2 r = fp2_dbl(fp2_sub(S2, S1));
-  const fp2 I = fp2_sqr_inl(fp2_dbl(H));
-  const fp2 J = fp2_mul_inl(H, I);
-  const fp2 V = fp2_mul_inl(U1, I);
-  const fp2 X3 = fp2_sub(fp2_sub(fp2_sqr_inl(r), J), fp2_dbl(V));
-  const fp2 Y3 = fp2_sub(fp2_mul_inl(r, fp2_sub(V, X3)), fp2_dbl(fp2_mul_inl(S1, J)));
-  const fp2 Z3 = fp2_mul_inl(fp2_sub(fp2_sub(fp2_sqr_inl(fp2_add(p.z, q.z)), Z1Z1), Z2Z2), H);
-  g2j out = {X3, Y3, Z3};
-  const bool pinf = jac_is_inf(p), qinf = jac_is_inf(q), h0 = fp2_is_zero(H);
-  if (pinf | qinf | h0) {  // per lane, rare
-    const bool r0 = fp2_is_zero(r);
-    out = pinf ? q : (qinf ? p : (r0 ? jac_dbl(p) : jac_infinity<fp2>()));
-  }
-  return out;
-}
-
+// additions are expanded in place too, with the base point re-read from staging at its uses.
 // madd-2007-bl (as jac_add_aff), q affine and never infinity
 DI g2j g2_madd_inl(const g2j& p, const g2a& q) {
   const fp2 Z1Z1 = fp2_sqr_inl(p.z);
@@ -376,42 +349,26 @@ DI g2j g2_madd_inl_exc(const g2j& p, QX qx, QY qy, const LdsFp2Slots& park, bool
   return {X3, Y3, park.get(1)};
 }
 
-// [|x|] P call-free; base() returns P again at each addition (affine for AFF: mixed additions)
-template <bool AFF, typename Base>
-DI g2j g2_mul_x_abs_inl(const g2j& p, Base base) {
+// [|x|] P call-free with mixed additions of the affine base() (re-read at each use); the exceptional
+// cases take g2_madd_inl's rarely executed branch. The generic fix-up kernels' form (k_decomp.hip
+// k_subgroup_g2_generic, g2_decompress with its subgroup check); the production chains are the
+// flagged programs of k_hash.hip / k_decomp.hip.
+template <typename Base>
+DI g2j g2_mul_x_abs_aff_inl(const g2j& p, Base base) {
   g2j acc = p;
 #pragma unroll 1
   for (int i = 62; i >= 0; i--) {
     acc = g2_dbl_inl(acc);
-    if ((BLS_X_ABS >> i) & 1ull) {
-      if constexpr (AFF)
-        acc = g2_madd_inl(acc, base());
-      else
-        acc = g2_add_inl(acc, base());
-    }
+    if ((BLS_X_ABS >> i) & 1ull) acc = g2_madd_inl(acc, base());
   }
   return acc;
 }
 
-#define G2_MUL_X_ABS_CHAIN g2_mul_x_abs_inl
-
 // g2_in_subgroup for an affine point re-read by `reload` (never infinity: the caller screens it)
 template <typename Reload>
 DI bool g2_in_subgroup_aff_reload(Reload reload) {
-  const g2j xp = jac_neg(G2_MUL_X_ABS_CHAIN<true>(jac_from_aff(reload()), reload));
+  const g2j xp = jac_neg(g2_mul_x_abs_aff_inl(jac_from_aff(reload()), reload));
   return jac_eq(g2_psi(jac_from_aff(reload())), xp);
-}
-
-// g2_clear_cofactor_reload with call-free chains: stash(A) parks A = [x]P + psi(P) (the second
-// chain's base) and reload_a() re-reads it
-template <typename Reload, typename Stash, typename ReloadA>
-DI g2j g2_clear_cofactor_inl(Reload reload, Stash stash, ReloadA reload_a) {
-  g2j a = jac_add(jac_neg(G2_MUL_X_ABS_CHAIN<false>(reload(), reload)), g2_psi(reload()));
-  stash(a);
-  g2j r = jac_add(jac_neg(G2_MUL_X_ABS_CHAIN<false>(a, reload_a)), jac_neg(reload_a()));
-  const g2j p = reload();
-  r = jac_add(r, jac_neg(p));
-  return jac_add(r, g2_psi2(jac_dbl(p)));
 }
 
 // RFC 9380 G.3 clear_cofactor_bls12381_g2: h_eff P = [x^2 - x - 1]P + [x - 1]psi(P) + psi^2(2P)
