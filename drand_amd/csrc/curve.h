@@ -150,8 +150,14 @@ DI bool jac_eq(const jac<F>& p, const jac<F>& q) {
 // the G2 cofactor clearing and subgroup check run their 63 doublings call-free, so the register
 // allocator sees the whole step instead of the AMDGPU call ABI's caller/callee-saved split.
 #define G2_DBL_FENCE() ((void)0)
+// the doubling's two products: Karatsuba where the unit asks for it (BLS_G2_DBL_KARA, default
+// BLS_FP2_KARA_INL); k_hash.hip keeps the dot form here, whose smaller working set lets its op
+// program enter and leave the doubling loop without spills
+#ifndef BLS_G2_DBL_KARA
+#define BLS_G2_DBL_KARA BLS_FP2_KARA_INL
+#endif
 DI g2j g2_dbl_inl(const g2j& p) {
-  const fp2 Z3 = fp2_dbl(fp2_mul_inl(p.y, p.z));
+  const fp2 Z3 = fp2_dbl(fp2_mul_inl_t<BLS_G2_DBL_KARA != 0>(p.y, p.z));
   G2_DBL_FENCE();
   const fp2 A = fp2_sqr_inl(p.x);
   G2_DBL_FENCE();
@@ -165,7 +171,7 @@ DI g2j g2_dbl_inl(const g2j& p) {
   const fp2 X3 = fp2_sub(fp2_sqr_inl(E), fp2_dbl(D));
   G2_DBL_FENCE();
   const fp2 C8 = fp2_dbl(fp2_dbl(fp2_dbl(C)));
-  const fp2 Y3 = fp2_sub(fp2_mul_inl(E, fp2_sub(D, X3)), C8);
+  const fp2 Y3 = fp2_sub(fp2_mul_inl_t<BLS_G2_DBL_KARA != 0>(E, fp2_sub(D, X3)), C8);
   return {X3, Y3, Z3};
 }
 

@@ -4,6 +4,9 @@
 // fp2_mul_inl): their live state leaves room for its extra operand arrays here, unlike the Miller
 // lines kernel (same-box A/B, profiles/r05_ab.json r05l: hash + decompression 100.7 -> 98.6 ms).
 #define BLS_FP2_KARA_INL 1
+#ifndef BLS_G2_DBL_KARA
+#define BLS_G2_DBL_KARA 0
+#endif
 #include "kcommon.h"
 
 namespace blsk {
@@ -38,7 +41,7 @@ DI void store_jac(uint32_t* Q, size_t cnt, size_t i, int slot, const g2j& p) {
 }
 
 #ifndef BLS_WPE_HASH_A
-#define BLS_WPE_HASH_A 4
+#define BLS_WPE_HASH_A 3
 #endif
 #ifndef BLS_WPE_HASH_B
 #define BLS_WPE_HASH_B 2
