@@ -721,9 +721,12 @@ int blsv_recover(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t*
 // collapse) and drops indices >= n; fewer than t distinct -> "not enough good public shares".
 // Lagrange at 0 over those t shares (x = index + 1) of the batch partials_stage just decompressed
 // into c->S, then the G2 MSM and compression.
-static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std::vector<uint32_t>& index, size_t lo,
-                        size_t hi, size_t t, size_t n, uint8_t* out_sig96) {
-  std::vector<uint32_t> sel, idx;
+// the shares recover_from interpolates: valid ones of [lo, hi) in input order until t are held, then
+// deduplicated by index and restricted to indices < n; false when fewer than t distinct remain
+static bool select_shares(const std::vector<uint8_t>& cls, const std::vector<uint32_t>& index, size_t lo, size_t hi,
+                          size_t t, size_t n, std::vector<uint32_t>& sel, std::vector<uint32_t>& idx) {
+  sel.clear();
+  idx.clear();
   size_t taken = 0;
   for (size_t i = lo; i < hi && taken < t; i++) {
     if (cls[i] != BLSV_REJ_OK) continue;
@@ -732,7 +735,13 @@ static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std:
     sel.push_back((uint32_t)i);
     idx.push_back(index[i]);
   }
-  if (sel.size() < t)
+  return sel.size() >= t;
+}
+
+static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std::vector<uint32_t>& index, size_t lo,
+                        size_t hi, size_t t, size_t n, uint8_t* out_sig96) {
+  std::vector<uint32_t> sel, idx;
+  if (!select_shares(cls, index, lo, hi, t, n, sel, idx))
     return fail(c, BLSV_ENOTENOUGH, "share: not enough good public shares to reconstruct secret commitment");
   HIPCHK(c, c->sel.ensure(t * 4));
   HIPCHK(c, c->idx.ensure(t * 4));
@@ -751,6 +760,92 @@ static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std:
   return BLSV_OK;
 }
 
+// Speculative recovery. A round's partials are all verified before recover_from picks its shares,
+// and the recovered signature is verified after: three latency launches in a row. The shares the
+// selection would pick if every partial verified are known before any verification, so they are
+// decoded (no subgroup check: validity is the partials' verdict), interpolated and compressed on the
+// side stream WHILE the partials verify on the main stream. The result is kept when the verdicts
+// leave the selection unchanged -- the same shares, hence the same bytes as recover_from -- and
+// recomputed by recover_from otherwise (a selected share failed). Only for rounds on the latency
+// path, whose partial verification leaves the side stream idle.
+struct SpecRecover {
+  bool launched = false;
+  std::vector<uint32_t> sel;  // round positions of the shares used
+};
+
+static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, size_t partial_len,
+                               const std::vector<uint32_t>& index, size_t lo, size_t hi, size_t t, size_t n,
+                               SpecRecover& sr) {
+  sr.launched = false;
+  std::vector<uint8_t> all_ok(index.size(), BLSV_REJ_OK);
+  std::vector<uint32_t> idx;
+  if (!select_shares(all_ok, index, lo, hi, t, n, sr.sel, idx)) return BLSV_OK;  // recover_from will say so
+  auto& sp = c->spec[slot];
+  const size_t tt = sr.sel.size();
+  const size_t host_need = tt * 96 + tt * 4 + tt * 4 + 128;
+  if (sp.host.sz < host_need) HIPCHK(c, hipStreamSynchronize(c->side));  // no copy may be pending on it
+  HIPCHK(c, sp.host.ensure(host_need));
+  uint8_t* h_sig = sp.host.as<uint8_t>();
+  uint32_t* h_idx = reinterpret_cast<uint32_t*>(h_sig + tt * 96);
+  uint32_t* h_sel = h_idx + tt;
+  for (size_t j = 0; j < tt; j++) {
+    std::memcpy(h_sig + j * 96, partials + (size_t)sr.sel[j] * partial_len + 2, 96);
+    h_idx[j] = idx[j];
+    h_sel[j] = (uint32_t)j;
+  }
+  HIPCHK(c, sp.sig.ensure(tt * 96));
+  HIPCHK(c, sp.S.ensure(tt * blsk::S_WORDS * 4));
+  HIPCHK(c, sp.s_inf.ensure(tt));
+  HIPCHK(c, sp.cls.ensure(tt));
+  HIPCHK(c, sp.sel.ensure(tt * 4));
+  HIPCHK(c, sp.idx.ensure(tt * 4));
+  HIPCHK(c, sp.lam.ensure(tt * 32));
+  HIPCHK(c, sp.scratch.ensure(tt * 192 * 4));
+  HIPCHK(c, sp.out.ensure(96));
+  hipStream_t st = c->side;
+  HIPCHK(c, hipMemcpyAsync(sp.sig.p, h_sig, tt * 96, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(sp.idx.p, h_idx, tt * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(sp.sel.p, h_sel, tt * 4, hipMemcpyHostToDevice, st));
+  blsk::launch_decompress_g2_only(sp.sig.as<uint8_t>(), 96, 0, tt, sp.S.as<uint32_t>(), sp.s_inf.as<uint8_t>(),
+                                  sp.cls.as<uint8_t>(), st);
+  blsk::launch_lagrange(sp.idx.as<uint32_t>(), (uint32_t)tt, sp.lam.as<uint32_t>(), st);
+  blsk::launch_lat_recover(sp.S.as<uint32_t>(), tt, sp.s_inf.as<uint8_t>(), sp.sel.as<uint32_t>(),
+                           sp.lam.as<uint32_t>(), (uint32_t)tt, sp.scratch.as<uint32_t>(), sp.out.as<uint8_t>(), st);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(h_sig + tt * 96 + tt * 8, sp.out.p, 96, hipMemcpyDeviceToHost, st));
+  sr.launched = true;
+  return BLSV_OK;
+}
+
+// after the partials' verdicts (cls): the speculative result if its selection stands, else
+// recover_from; the side stream is drained either way
+static int spec_recover_finish(blsv_ctx* c, int slot, const SpecRecover& sr, const std::vector<uint8_t>& cls,
+                               const std::vector<uint32_t>& index, size_t lo, size_t hi, size_t t, size_t n,
+                               uint8_t* out_sig96) {
+  if (sr.launched) {
+    HIPCHK(c, hipStreamSynchronize(c->side));
+    std::vector<uint32_t> sel, idx;
+    if (select_shares(cls, index, lo, hi, t, n, sel, idx) && sel == sr.sel) {
+      const size_t tt = sr.sel.size();
+      std::memcpy(out_sig96, c->spec[slot].host.as<uint8_t>() + tt * 96 + tt * 8, 96);
+      c->spec_hits++;
+      return BLSV_OK;
+    }
+    c->spec_misses++;
+  }
+  return recover_from(c, cls, index, lo, hi, t, n, out_sig96);
+}
+
+// partial_len == 98 and the round small enough for the latency path (partials_stage's choice)
+static bool spec_applies(const blsv_ctx* c, size_t k, size_t partial_len) {
+  return partial_len == 98 && c->has_group && k > 0 && k <= std::min(c->lat_max, c->chunk);
+}
+
+static void share_indices(const uint8_t* partials, size_t partial_len, size_t k, std::vector<uint32_t>& index) {
+  index.assign(k, 0);
+  for (size_t i = 0; i < k; i++) index[i] = ((uint32_t)partials[i * partial_len] << 8) | partials[i * partial_len + 1];
+}
+
 int blsv_aggregate(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
                    size_t k, size_t t, size_t n, uint8_t* ok, uint8_t* reject_class, uint8_t* out_sig96,
                    uint8_t* group_ok) {
@@ -760,14 +855,23 @@ int blsv_aggregate(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_
   (void)hipSetDevice(c->device);
   std::vector<uint8_t> cls;
   std::vector<uint32_t> index;
+  SpecRecover sr;
+  if (spec_applies(c, k, partial_len)) {
+    share_indices(partials, partial_len, k, index);
+    int rc0 = spec_recover_launch(c, 0, partials, partial_len, index, 0, k, t, n, sr);
+    if (rc0) return rc0;
+  }
   int rc = partials_stage(c, msg, msg_len, partials, partial_len, k, cls, index);
-  if (rc) return rc;
+  if (rc) {
+    if (sr.launched) (void)hipStreamSynchronize(c->side);
+    return rc;
+  }
   for (size_t i = 0; i < k; i++) {
     ok[i] = cls[i] == BLSV_REJ_OK;
     if (reject_class) reject_class[i] = cls[i];
   }
   *group_ok = 0;
-  rc = recover_from(c, cls, index, 0, k, t, n, out_sig96);
+  rc = spec_recover_finish(c, 0, sr, cls, index, 0, k, t, n, out_sig96);
   if (rc) return rc;
   // VerifyRecovered(group key, msg, sig) (chain/beacon/chain.go:141)
   const uint32_t len = (uint32_t)msg_len;
@@ -808,18 +912,34 @@ int blsv_aggregate_round(blsv_ctx* c, const uint8_t* msg1, size_t msg1_len, cons
   if (k2) parts.insert(parts.end(), partials2, partials2 + k2 * partial_len);
   std::vector<uint8_t> cls;
   std::vector<uint32_t> index;
+  const bool try_v2 = k2 >= t;
+  SpecRecover sr1, sr2;  // both recoveries speculated on the side stream (see spec_recover_launch)
+  if (spec_applies(c, k, partial_len)) {
+    share_indices(parts.data(), partial_len, k, index);
+    int rc0 = spec_recover_launch(c, 0, parts.data(), partial_len, index, 0, k1, t, n, sr1);
+    if (!rc0 && try_v2) rc0 = spec_recover_launch(c, 1, parts.data(), partial_len, index, k1, k, t, n, sr2);
+    if (rc0) {
+      (void)hipStreamSynchronize(c->side);
+      return rc0;
+    }
+  }
   int rc = partials_stage(c, msgs.data(), 0, parts.data(), partial_len, k, cls, index, lens.data());
-  if (rc) return rc;
+  if (rc) {
+    if (sr1.launched || sr2.launched) (void)hipStreamSynchronize(c->side);
+    return rc;
+  }
   for (size_t i = 0; i < k1; i++) ok1[i] = cls[i] == BLSV_REJ_OK;
   for (size_t i = 0; i < k2; i++) ok2[i] = cls[k1 + i] == BLSV_REJ_OK;
   // Recover V1 (chain.go:136) and, with LenV2 >= thr, V2 (chain.go:153-155) from the staged shares
-  rc = recover_from(c, cls, index, 0, k1, t, n, sig1_96);
-  if (rc == BLSV_ENOTENOUGH) return BLSV_OK;  // "invalid_recovery": no beacon this time
+  rc = spec_recover_finish(c, 0, sr1, cls, index, 0, k1, t, n, sig1_96);
+  if (rc == BLSV_ENOTENOUGH) {
+    if (sr2.launched) (void)hipStreamSynchronize(c->side);
+    return BLSV_OK;  // "invalid_recovery": no beacon this time
+  }
   if (rc) return rc;
-  const bool try_v2 = k2 >= t;
   bool v2_recovered = false;
   if (try_v2) {
-    rc = recover_from(c, cls, index, k1, k, t, n, sig2_96);
+    rc = spec_recover_finish(c, 1, sr2, cls, index, k1, k, t, n, sig2_96);
     if (rc && rc != BLSV_ENOTENOUGH) return rc;
     v2_recovered = rc == BLSV_OK;
   }
@@ -961,6 +1081,13 @@ int blsv_profile_read(blsv_ctx* c, double* ms, uint64_t* launches, uint64_t* ite
   }
   c->recs.clear();
   return ST_N;
+}
+
+int blsv_test_spec_stats(blsv_ctx* c, uint64_t* hits, uint64_t* misses) {
+  if (!c || !hits || !misses) return BLSV_EINVAL;
+  *hits = c->spec_hits;
+  *misses = c->spec_misses;
+  return BLSV_OK;
 }
 
 int blsv_test_generic_chains(blsv_ctx* c, int on) {

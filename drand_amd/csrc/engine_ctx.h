@@ -178,6 +178,13 @@ struct blsv_ctx {
       pp_tab, pp_inf, sel, g1_cls, misc;
   // one packed upload / download per service batch (svc_verify_mixed)
   PinBuf pin;
+  // speculative recovery beside a round's partial verification (blsverify.cpp spec_recover_*): two
+  // slots (V1, V2), each with its decoded shares, Lagrange coefficients, products and output
+  struct SpecSlot {
+    DBuf sig, S, s_inf, cls, sel, idx, lam, scratch, out;
+    PinBuf host;  // staged sigma bytes + indices in, the 96-byte result out (async copies only)
+  } spec[2];
+  uint64_t spec_hits = 0, spec_misses = 0;  // speculative recoveries kept / recomputed
   DBuf arena;
 };
 

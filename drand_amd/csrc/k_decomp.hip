@@ -129,6 +129,15 @@ void launch_decompress_g2(const uint8_t* sigs, size_t stride, size_t offset, siz
                      g_generic_chains_all);
 }
 
+// decoding only (no subgroup check): the speculative recovery's shares, whose validity the round's
+// own partial verification decides (blsverify.cpp spec_recover_launch)
+void launch_decompress_g2_only(const uint8_t* sigs, size_t stride, size_t offset, size_t cnt, uint32_t* S,
+                               uint8_t* s_inf, uint8_t* cls, hipStream_t st) {
+  if (!cnt) return;
+  hipLaunchKernelGGL(k_decompress_g2, dim3(grid_for(cnt)), dim3(TPB), 0, st, sigs, stride, offset, size_t(0), cnt, S,
+                     s_inf, cls);
+}
+
 void launch_finish(const uint8_t* cls, size_t base, size_t cnt, uint64_t* bitmap, unsigned long long* first_bad,
                    uint64_t label0, hipStream_t st) {
   if (!cnt) return;

@@ -373,6 +373,12 @@ class Engine:
                                                   inf))
         return list(O)[:n * 48], list(inf)[:n]
 
+    def spec_stats(self):
+        """(kept, recomputed) speculative recoveries of this context (blsv_test_spec_stats)."""
+        h, m = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self.lib.blsv_test_spec_stats(self._h, ctypes.byref(h), ctypes.byref(m)))
+        return h.value, m.value
+
     def test_generic_chains(self, on=True):
         """Every hash's cofactor clearing and every signature's subgroup check through the generic
         formulas (k_hash_cofactor_generic, k_subgroup_g2_generic) instead of only the lanes the

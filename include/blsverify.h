@@ -30,7 +30,9 @@
  *    workgroup of eight waves per item, every limb of a field element in its own lane
  *    (drand_amd/csrc/k_lat.hip). Measured on MI355X (profiles/r05r_latency.json, warm): one
  *    VerifyRecovered 2.3 ms; blsv_aggregate of an n = 64 / t = 33 round (64 VerifyPartial +
- *    Recover + VerifyRecovered) 6.8 ms. Up to 256 items the time stays ~2.5 ms (every item has its
+ *    Recover + VerifyRecovered) 5.6 ms (profiles/r05t_latency.json: the recovery of the shares
+ *    the round would select if all verify runs beside the partial verification and is kept when
+ *    the verdicts confirm that selection). Up to 256 items the time stays ~2.5 ms (every item has its
  *    own CU), then grows ~2.35 ms per further 256 items (profiles/r05r_latency_sweep.json).
  *  - Larger calls run on the BATCH pipeline (one lane per item, staged kernels): ~15 ms floor
  *    (14.2 ms at 64 items, 15.4 ms at 2,048: profiles/r05r_latency_sweep.json), then ~0.43 us per

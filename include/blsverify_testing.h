@@ -42,6 +42,13 @@ int blsv_test_hash_to_g2(blsv_ctx* ctx, const uint8_t* msgs, const uint32_t* msg
 int blsv_test_generic_chains(blsv_ctx* ctx, int on);
 
 /*
+ * Speculative recoveries of this context (blsv_aggregate / blsv_aggregate_round on the latency path):
+ * hits = kept (the partials' verdicts left the speculated share selection unchanged), misses =
+ * recomputed after a selected share failed.
+ */
+int blsv_test_spec_stats(blsv_ctx* ctx, uint64_t* hits, uint64_t* misses);
+
+/*
  * Stage timing for bench.py's roofline: when enabled, every stage launch (0 hash, 1 decompress,
  * 2 miller, 3 final_exp, 4 finish, 5 lat = a whole batch on the latency path) is bracketed by HIP
  * events on its launch stream. blsv_profile_read waits for the recorded events, writes per-stage

@@ -125,11 +125,27 @@ def test_aggregate_round(engine, golden):
     engine.set_group([bytes.fromhex(c) for c in th["commits"]], th["n"])
     msg = bytes.fromhex(th["msg"])
     partials = [bytes.fromhex(p) for p in th["partials"]]
+    # the recovery is speculated beside the partials' verification (blsverify.cpp spec_recover_*):
+    # kept when every selected share verifies, recomputed from the valid shares otherwise
+    h0, m0 = engine.spec_stats()
     ok, cls, sig, gok = engine.aggregate(msg, partials, th["t"], th["n"])
     assert all(ok) and gok and sig.hex() == th["group_sig"]
+    assert engine.spec_stats() == (h0 + 1, m0)
     bad = bytes.fromhex(th["bad_partial"])
+    # the golden bad share repeats index 3: assumed valid it would leave only 32 distinct indices
+    # among the first 33 shares, so nothing is speculated and the sequential recovery runs
     ok, cls, sig, gok = engine.aggregate(msg, [bad] + partials[:th["t"]], th["t"], th["n"])
     assert ok[0] is False and all(ok[1:]) and gok and sig.hex() == th["group_sig"]
+    assert engine.spec_stats() == (h0 + 1, m0)
+    # share 0 with a flipped signature bit: speculated, fails verification, recomputed from 1..33
+    flip = partials[0][:40] + bytes([partials[0][40] ^ 1]) + partials[0][41:]
+    ok, cls, sig, gok = engine.aggregate(msg, [flip] + partials[1:th["t"] + 1], th["t"], th["n"])
+    assert ok[0] is False and all(ok[1:]) and gok and sig.hex() == th["group_sig"]
+    assert engine.spec_stats() == (h0 + 1, m0 + 1)
+    # a bad share after the first t: the speculated selection stands
+    ok, cls, sig, gok = engine.aggregate(msg, partials[:th["t"]] + [flip], th["t"], th["n"])
+    assert all(ok[:-1]) and ok[-1] is False and gok and sig.hex() == th["group_sig"]
+    assert engine.spec_stats() == (h0 + 2, m0 + 1)
     with pytest.raises(EngineError):
         engine.aggregate(msg, [bad] + partials[:th["t"] - 1], th["t"], th["n"])
 
