@@ -160,9 +160,10 @@ WVI V mont_reduce(V64 T) {
   // first carry round in 64 bits (the carry may exceed 32 bits), then 32-bit rounds
   const V64 c = T >> 25;
   const V64 x64 = add64(widen(lo32(T) & M25), join64(wave_shr1(lo32(c)), wave_shr1(hi32(c))));  // < 2^34
-  V x = (lo32(x64) & M25) + wave_shr1(shr64_lo(x64, 25));  // < 2^25 + 2^9
-  x = norm1(x);                                            // < 2^25 + 2
-  // m = x * N' mod R: four independent MAD chains (a single chain would pay the MAD latency 16 times)
+  // < 2^25 + 2^9: enough for both products below (16 x (2^25 + 2^9) 2^25 < 2^55 in m's columns, and
+  // x only seeds U's 64-bit accumulator)
+  const V x = (lo32(x64) & M25) + wave_shr1(shr64_lo(x64, 25));
+  // m = x * N' mod R
   V64 ma[4] = {vsplat64(0), vsplat64(0), vsplat64(0), vsplat64(0)};
   sfor<16>([&](auto J) { ma[J & 3] = mad(row_shr<J>(x), NP25[J], ma[J & 3]); });
   const V64 mm = add64(add64(ma[0], ma[1]), add64(ma[2], ma[3]));  // columns < 2^55
@@ -175,11 +176,11 @@ WVI V mont_reduce(V64 T) {
   V y = (lo32(u) & M25) + wave_shr1(shr64_lo(u, 25));
   y = norm1(y);
   y = norm1(y);  // limbs in [0, 2^25]
-  // the even row now holds 0 or exactly R: carry one into the odd row's first limb when nonzero
-  const uint64_t nz = ballot(y != 0u) & 0x0000FFFF0000FFFFull;
-  const uint32_t c0 = (nz & 0xFFFFull) != 0, c1 = (nz >> 32) != 0;
+  // the even row now holds 0 or exactly R: carry one into the odd row's first limb when nonzero. Limbs
+  // up to 2^25 below the top one sum to less than 2^400, so R has a nonzero top limb (lane 15 / 47)
+  // and 0 does not: lanes 16 and 48 test their wave neighbour, no ballot
   const V l = lane_id();
-  y = y + sel(l == 16u, vsplat(c0), sel(l == 48u, vsplat(c1), vsplat(0)));
+  y = y + sel(((l & 0x1Fu) == 16u) & (wave_shr1(y) != 0u), vsplat(1), vsplat(0));
   return pl16_swap(y, vsplat(0)).b;  // odd rows -> even rows, odd rows zero
 }
 
@@ -188,13 +189,12 @@ WVI V win_off() {
   const V l = lane_id();
   return L_WIN + (l >> 5) * 48u + 16u + (l & 31u);
 }
-// stage term s: window <- a, broadcast <- b (and its negation D - b for an Fp2 term)
-WVI void stage_term(int s, V a, V b, bool fp2) {
+// stage term s: window <- a, broadcast <- b (an Fp2 term also stores D - b, dot_body)
+WVI void stage_term(int s, V a, V b) {
   uint32_t* lds = wave_lds() + s * SLOT_WORDS;
   const V l = lane_id();
   lds_st(lds, win_off(), a);
   lds_st(lds, L_BX + l, b);
-  if (fp2) lds_st(lds, L_BZ + l, hword(WC_DMUL) - b);
 }
 // Fp2 term s into the accumulators (two chains per component): half 0 -> a0 b0 | a0 b1,
 // half 1 -> a1 (D - b1) | a1 b0
@@ -230,8 +230,13 @@ template <int N>
 WVI V dot_body(const V (&a)[N], const V (&b)[N]) {
   static_assert(N >= 1 && N <= MAX_TERMS, "dot terms");
   WV_COUNT(OPC_DOT1 + N - 1);
+  // D read once and first: the windows and broadcasts are stored while it is in flight, the negations
+  // after it returns (one LDS round trip instead of one per term)
+  const V dm = hword(WC_DMUL);
 #pragma unroll
-  for (int i = 0; i < N; i++) stage_term(i, a[i], b[i], true);
+  for (int i = 0; i < N; i++) stage_term(i, a[i], b[i]);
+#pragma unroll
+  for (int i = 0; i < N; i++) lds_st(wave_lds() + i * SLOT_WORDS, L_BZ + lane_id(), dm - b[i]);
   wsync();
   V64 s1[2] = {vsplat64(0), vsplat64(0)}, s2[2] = {vsplat64(0), vsplat64(0)};
 #pragma unroll
@@ -274,7 +279,7 @@ WV_NOINL V dot6_v(V a0, V b0, V a1, V b1, V a2, V b2, V a3, V b3, V a4, V b4, V 
 // pair product [a0 b0 | a1 b1]
 WV_NOINL V mulp_v(V a, V b) {
   WV_COUNT(OPC_MULP);
-  stage_term(0, a, b, false);
+  stage_term(0, a, b);
   wsync();
   V64 s[4] = {vsplat64(0), vsplat64(0), vsplat64(0), vsplat64(0)};
   acc_pair(0, s);
@@ -288,7 +293,7 @@ WV_NOINL V sqr2_v(V a) {
   const VP d = pl32_swap(a, a);  // .a = [a0 | a0], .b = [a1 | a1]
   const V u = d.a + sel(h0, d.b, d.a);
   const V v = norm1(sel(h0, d.a + hword(WC_DMUL) - d.b, d.b));
-  stage_term(0, u, v, false);
+  stage_term(0, u, v);
   wsync();
   V64 s[4] = {vsplat64(0), vsplat64(0), vsplat64(0), vsplat64(0)};
   acc_pair(0, s);
@@ -298,7 +303,7 @@ WV_NOINL V sqr2_v(V a) {
 // Fp2 norm a0^2 + a1^2 in both halves: one pair product, halves summed, one reduction
 WV_NOINL V norm_dup_v(V a) {
   WV_COUNT(OPC_NORM);
-  stage_term(0, a, a, false);
+  stage_term(0, a, a);
   wsync();
   V64 s4[4] = {vsplat64(0), vsplat64(0), vsplat64(0), vsplat64(0)};
   acc_pair(0, s4);

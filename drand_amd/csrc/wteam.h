@@ -20,6 +20,10 @@
 
 namespace wv {
 
+// the polling waves' back-off between counter reads (s_sleep units of 64 clocks; 0: none)
+#ifndef WV_POLL_SLEEP
+#define WV_POLL_SLEEP 0
+#endif
 #ifndef WV_BLK_SLOTS
 #define WV_BLK_SLOTS 128
 #endif
@@ -103,7 +107,7 @@ WVI void team_sync(Team& t) {
   if (threadIdx.x % 64 == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) <
          target)
-    __builtin_amdgcn_s_sleep(1);
+    if (WV_POLL_SLEEP) __builtin_amdgcn_s_sleep(WV_POLL_SLEEP);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #endif
 }
@@ -136,7 +140,7 @@ WVI void flag_wait(int ctr, uint32_t count) {
 #else
   uint32_t* c = blk_base() + BLK_SLOTS * 64 + BLK_WORDS_EXTRA + ctr;
   while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < count)
-    __builtin_amdgcn_s_sleep(1);
+    if (WV_POLL_SLEEP) __builtin_amdgcn_s_sleep(WV_POLL_SLEEP);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #endif
 }

@@ -275,7 +275,9 @@ WVI V row_shl(V x) {
 }
 template <int i>
 WVI V row_bcast(V x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150 + i, 0xf, 0xf, false);
+  // every lane is written (all rows and banks, an in-row source), so no "old" value: mov_dpp leaves it
+  // undefined and the compiler does not zero the destination first
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + i, 0xf, 0xf, false);
 }
 WVI V wave_shr1(V x) { return WV_DPP(x, 0x138); }
 struct VP {

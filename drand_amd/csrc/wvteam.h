@@ -260,7 +260,8 @@ constexpr int DEC_POWS = 2;   // whash.h g2_decompress (none when it rejects bef
 // wcurve.h g2_dbl (dbl-2009-l) in three rounds of one product per wave, on the accumulator's slots:
 // A = X^2, B = Y^2, Z3 = 2 Y Z | C = B^2, D = 4 X B, EE = (3A)^2 | X3 = E^2 - 2D, Y3 = E (3D - EE) - 8C
 // (Y3 = E (D - X3) - 8C with X3 substituted, so X3 and Y3 are one round)
-WVI void team_g2_dbl(Team& t, int acc) {
+// rounds 1 and 2 (A, B, Z3 | C, D, EE), shared with team_g2_dbl2
+WVI void team_g2_dbl_r12(Team& t, int acc) {
   for (int j = t.id; j < 3; j += t.n) {
     const F Y = xld(acc + 1);
     if (j == 0) xst(HS_A, sqr2(xld(acc)));
@@ -275,10 +276,53 @@ WVI void team_g2_dbl(Team& t, int acc) {
     else xst(HS_EE, sqr2(mul_small<3>(xld(HS_A))));
   }
   team_sync(t);
+}
+WVI void team_g2_dbl(Team& t, int acc) {
+  team_g2_dbl_r12(t, acc);
   for (int j = t.id; j < 2; j += t.n) {
     const F E = mul_small<3>(xld(HS_A)), D = xld(HS_D);
     if (j == 0) xst(acc, dot(E, E, D, cst(WC_NEG2)));
     else xst(acc + 1, dot(sub<0>(mul_small<3>(D), xld(HS_EE)), E, xld(HS_C), cst(WC_NEG8)));
+  }
+  team_sync(t);
+}
+// two doublings in five rounds instead of six. The first as above, except that X3 = EE - 2D is left as
+// that linear form; the second from (X3, Y3, Z3) with A' = X3^2 as dbl-2009-l, written in products of
+// the earlier rounds' outputs:
+//   X5 = 9 A'^2 - 8 X3 B',  Y5 = 36 X3^3 B' - 27 (X3^3)^2 - 8 B'^2 = X3^3 (36 B' - 27 X3^3) - 8 B'^2,
+//   Z5 = 2 Y3 Z3  (B' = Y3^2, X3^3 = A' X3)
+// -- the same polynomials as two team_g2_dbl calls, so the same Jacobian coordinates:
+//   A, B, Z3 | C, D, EE | Y3, A' | X3^3, B', Z5 | X5, Y5
+// (Y's slot takes Y3 and Z's Z3 then Z5; A' goes to B's slot, X3^3 to C's, B' to A's, each after its
+// last read)
+WVI void team_g2_dbl2(Team& t, int acc) {
+  team_g2_dbl_r12(t, acc);
+  auto x3 = [&]() { return sub<0>(xld(HS_EE), dbl(xld(HS_D))); };  // X3 = EE - 2D (bound 5 p)
+  for (int j = t.id; j < 2; j += t.n) {
+    if (j == 0) {
+      const F E = mul_small<3>(xld(HS_A)), D = xld(HS_D);
+      xst(acc + 1, dot(sub<0>(mul_small<3>(D), xld(HS_EE)), E, xld(HS_C), cst(WC_NEG8)));
+    } else {
+      xst(HS_B, sqr2(x3()));
+    }
+  }
+  team_sync(t);
+  for (int j = t.id; j < 3; j += t.n) {
+    const F Y3 = xld(acc + 1);
+    if (j == 0) xst(HS_C, dot(xld(HS_B), x3()));
+    else if (j == 1) xst(HS_A, sqr2(Y3));
+    else xst(acc + 2, dot(dbl(Y3), xld(acc + 2)));
+  }
+  team_sync(t);
+  for (int j = t.id; j < 2; j += t.n) {
+    const F Bp = xld(HS_A), n8B = mul_small<8>(neg<0>(Bp));
+    if (j == 0) {
+      const F Ap = xld(HS_B);
+      xst(acc, dot(Ap, mul_small<9>(Ap), x3(), n8B));
+    } else {
+      const F X33 = xld(HS_C);
+      xst(acc + 1, dot(X33, sub<1>(mul_small<36>(Bp), mul_small<27>(X33)), Bp, n8B));
+    }
   }
   team_sync(t);
 }
@@ -348,10 +392,26 @@ WVI void team_mul_x_abs(Team& t, int base, int acc) {
     xst_word(XW_BINF, is_zero2(Z2) ? 1u : 0u);
   }
   team_sync(t);
+  // the runs of doublings between the additions (1, 2, 3, 9, 32, 16 for |x|) in pairs, an odd run's
+  // last doubling alone
+  int i = 62;
 #pragma unroll 1
-  for (int i = 62; i >= 0; i--) {
-    team_g2_dbl(t, acc);
-    if ((bls::BLS_X_ABS >> i) & 1ull) team_g2_add_fixed(t, acc, base);
+  while (i >= 0) {
+    int run = 1;
+    while (i - run >= 0 && !((bls::BLS_X_ABS >> (i - run + 1)) & 1ull)) run++;  // bits i .. i-run+1
+#ifndef WV_DBL2
+#define WV_DBL2 1
+#endif
+    if (WV_DBL2) {
+#pragma unroll 1
+      for (int k = 0; k + 1 < run; k += 2) team_g2_dbl2(t, acc);
+      if (run & 1) team_g2_dbl(t, acc);
+    } else {
+#pragma unroll 1
+      for (int k = 0; k < run; k++) team_g2_dbl(t, acc);
+    }
+    i -= run;
+    if ((bls::BLS_X_ABS >> (i + 1)) & 1ull) team_g2_add_fixed(t, acc, base);
   }
 }
 // acc <- acc + base for any two points (wcurve.h g2_add) in five rounds, the base's Z powers included:

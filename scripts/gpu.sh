@@ -21,6 +21,7 @@
 #   variant:NAME     GPU suite + bench on variants/libblsverify_NAME.so (scripts/build_variant.sh,
 #                    loaded through DRAND_AMD_LIB)
 #   vbench:NAME      bench only on that variant (same-box A/B against a plain `bench` step)
+#   vlat:NAME        tools/latency_bench.py on that variant (same-box A/B against a plain `lat` step)
 set -o pipefail
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 2
@@ -86,6 +87,13 @@ for step in "$@"; do
         DRAND_AMD_LIB=$L timeout -k 10 900 $PYT > "$O/pytest_gpu_$V.log" 2>&1 &&
         DRAND_AMD_LIB=$L timeout -k 10 400 python -u bench.py --cpu-per-worker 0 > "$O/bench_$V.json" \
           2> "$O/bench_$V.err" || rc=31
+      fi ;;
+    vlat:*)
+      V=${step#vlat:}
+      L=variants/libblsverify_$V.so
+      if [ ! -f "$L" ]; then echo "no $L"; rc=30; else
+        DRAND_AMD_LIB=$L timeout -k 10 300 python -u tools/latency_bench.py --reps 10 --out "$O/latency_$V.json" \
+          > "$O/latency_$V.log" 2>&1 || rc=32
       fi ;;
     vbench:*)
       V=${step#vbench:}
