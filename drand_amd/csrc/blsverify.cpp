@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
@@ -55,6 +56,62 @@ int ensure_workspace(blsv_ctx* c, size_t cnt) {
     c->lat_max = std::min(c->lat_max, c->chunk);
     c->oom_halvings++;
   }
+}
+
+// Small copies on the main stream go through pinned staging: hipMemcpyAsync from pageable memory is
+// staged by the runtime and costs ~10 us per copy, which is most of a lone verify's host time.
+// Uploads are copied into io_up (the caller's buffer is free on return) and DMA'd from there; the
+// staging is appended to and reused from offset 0 only after a synchronisation of the stream, so no
+// copy still in flight is overwritten. Downloads land in io_down and reach the caller's buffers after
+// the synchronisation download_sync itself does. Larger copies take the pageable path as before.
+constexpr size_t kIoCap = size_t(1) << 20;
+
+static hipError_t h2d(blsv_ctx* c, void* dst, const void* src, size_t len) {
+  if (!len) return hipSuccess;
+  if (len > kIoCap / 4) return hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, c->stream);
+  if (!c->io_up.p) {
+    hipError_t e = c->io_up.ensure(kIoCap);
+    if (e != hipSuccess) return e;
+  }
+  if (c->io_up_off + len > kIoCap) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return e;
+    c->io_up_off = 0;
+  }
+  uint8_t* h = c->io_up.as<uint8_t>() + c->io_up_off;
+  memcpy(h, src, len);
+  c->io_up_off += (len + 63) & ~size_t(63);
+  return hipMemcpyAsync(dst, h, len, hipMemcpyHostToDevice, c->stream);
+}
+
+struct Down {
+  void* user;
+  const void* dev;
+  size_t len;
+};
+// every download enqueued, one synchronisation of the main stream, then the bytes to the callers
+static hipError_t download_sync(blsv_ctx* c, std::initializer_list<Down> ds) {
+  size_t total = 0;
+  for (const Down& d : ds) total += (d.len + 63) & ~size_t(63);
+  const bool staged = total <= kIoCap && (c->io_down.p || c->io_down.ensure(kIoCap) == hipSuccess);
+  hipError_t e = hipSuccess;
+  size_t off = 0;
+  for (const Down& d : ds) {
+    if (!d.len) continue;
+    void* to = staged ? (void*)(c->io_down.as<uint8_t>() + off) : d.user;
+    if (e == hipSuccess) e = hipMemcpyAsync(to, d.dev, d.len, hipMemcpyDeviceToHost, c->stream);
+    off += (d.len + 63) & ~size_t(63);
+  }
+  const hipError_t es = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = es;
+  if (e == hipSuccess) c->io_up_off = 0;  // every staged upload has completed too
+  if (e != hipSuccess || !staged) return e;
+  off = 0;
+  for (const Down& d : ds) {
+    if (d.len) memcpy(d.user, c->io_down.as<uint8_t>() + off, d.len);
+    off += (d.len + 63) & ~size_t(63);
+  }
+  return hipSuccess;
 }
 
 static hipEvent_t take_event(blsv_ctx* c) {
@@ -251,10 +308,9 @@ static int verify_driver(blsv_ctx* c, size_t n, const uint8_t* d_sigs, size_t st
   }
   std::vector<uint64_t> w(words + 1, 0);
   uint64_t fb = UINT64_MAX;
-  if (words) HIPCHK(c, hipMemcpyAsync(w.data(), c->bitmap.p, words * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(&fb, c->first_bad.p, 8, hipMemcpyDeviceToHost, c->stream));
-  if (reject_class && n) HIPCHK(c, hipMemcpyAsync(reject_class, c->misc.p, n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, download_sync(c, {{w.data(), c->bitmap.p, words * 8},
+                              {&fb, c->first_bad.p, 8},
+                              {reject_class, c->misc.p, reject_class ? n : 0}}));
   if (ok_bitmap) bitmap_words_to_bytes(w, n, ok_bitmap);
   if (first_bad_idx) *first_bad_idx = fb;
   return BLSV_OK;
@@ -285,11 +341,12 @@ static int upload_messages(blsv_ctx* c, const uint8_t* msgs, const uint32_t* msg
   HIPCHK(c, c->in_msgs.ensure(off[n] + 1));
   HIPCHK(c, c->in_off.ensure((n + 1) * 8));
   HIPCHK(c, c->in_len.ensure(n * 4 + 4));
-  if (off[n]) HIPCHK(c, hipMemcpyAsync(c->in_msgs.p, msgs, off[n], hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->in_off.p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->in_len.p, msg_lens, n * 4, hipMemcpyHostToDevice, c->stream));
-  // keep the host vectors alive until the copies complete
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const size_t staged_max = kIoCap / 4;
+  HIPCHK(c, h2d(c, c->in_msgs.p, msgs, off[n]));
+  HIPCHK(c, h2d(c, c->in_off.p, off.data(), (n + 1) * 8));
+  HIPCHK(c, h2d(c, c->in_len.p, msg_lens, n * 4));
+  // a pageable copy of the offsets reads them when it runs: keep the vector alive until then
+  if ((n + 1) * 8 > staged_max) HIPCHK(c, hipStreamSynchronize(c->stream));
   return BLSV_OK;
 }
 
@@ -433,8 +490,8 @@ int blsv_verify_chained(blsv_ctx* c, uint64_t first_round, const uint8_t* prev0,
   HIPCHK(c, c->in_sigs.ensure(n * 96 + 96));
   HIPCHK(c, c->seeds.ensure(96));
   if (n) {
-    HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, sigs96, n * 96, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->seeds.p, prev0, prev0_len, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, h2d(c, c->in_sigs.p, sigs96, n * 96));
+    HIPCHK(c, h2d(c, c->seeds.p, prev0, prev0_len));
   }
   blsk::ChainedSrc src{c->in_sigs.as<uint8_t>(), c->seeds.as<uint8_t>(), first_round, std::max<uint64_t>(n, 1),
                        (uint32_t)prev0_len};
@@ -463,8 +520,8 @@ int blsv_verify_prevs(blsv_ctx* c, uint64_t first_round, const uint8_t* prevs96,
   HIPCHK(c, c->in_sigs.ensure(n * 96 + 96));
   HIPCHK(c, c->seeds.ensure(n * 96 + 96));
   if (n) {
-    HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, sigs96, n * 96, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->seeds.p, prevs96, n * 96, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, h2d(c, c->in_sigs.p, sigs96, n * 96));
+    HIPCHK(c, h2d(c, c->seeds.p, prevs96, n * 96));
   }
   // segments of length 1: every round hashes its own prev row (seeds[i]); row 0 uses prev0_len bytes
   blsk::ChainedSrc src{c->in_sigs.as<uint8_t>(), c->seeds.as<uint8_t>(), first_round, 1, (uint32_t)prev0_len};
@@ -489,11 +546,11 @@ int blsv_verify_unchained(blsv_ctx* c, const uint64_t* rounds, uint64_t first_ro
   if (n && !sigs96) return fail(c, BLSV_EINVAL, "verify_unchained: null signatures");
   (void)hipSetDevice(c->device);
   HIPCHK(c, c->in_sigs.ensure(n * 96 + 96));
-  if (n) HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, sigs96, n * 96, hipMemcpyHostToDevice, c->stream));
+  if (n) HIPCHK(c, h2d(c, c->in_sigs.p, sigs96, n * 96));
   const uint64_t* d_rounds = nullptr;
   if (rounds && n) {
     HIPCHK(c, c->in_rounds.ensure(n * 8));
-    HIPCHK(c, hipMemcpyAsync(c->in_rounds.p, rounds, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, h2d(c, c->in_rounds.p, rounds, n * 8));
     d_rounds = c->in_rounds.as<uint64_t>();
   }
   uint64_t fb = UINT64_MAX;
@@ -539,7 +596,7 @@ int blsv_verify_messages(blsv_ctx* c, const uint8_t* pk48, const uint8_t* msgs, 
   int rc = upload_messages(c, msgs, msg_lens, n);
   if (rc) return rc;
   HIPCHK(c, c->in_sigs.ensure(n * 96 + 96));
-  if (n) HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, sigs96, n * 96, hipMemcpyHostToDevice, c->stream));
+  if (n) HIPCHK(c, h2d(c, c->in_sigs.p, sigs96, n * 96));
   return verify_driver(
       c, n, c->in_sigs.as<uint8_t>(), 96, 0, pk,
       [&](size_t base, size_t cnt) {
@@ -619,7 +676,7 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
   }
   if (rc) return rc;
   HIPCHK(c, c->idx.ensure(k * 4));
-  HIPCHK(c, hipMemcpyAsync(c->idx.p, index.data(), k * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, h2d(c, c->idx.p, index.data(), k * 4));
   // PubPoly.Eval(index): the per-group table when every index is a member index (< n), else
   // evaluated for this batch (an index >= n still has a well-defined Eval in kyber)
   bool in_table = true;
@@ -632,13 +689,13 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
     HIPCHK(c, c->sel.ensure(k * 4));
     ident.resize(k);
     for (size_t i = 0; i < k; i++) ident[i] = (uint32_t)i;
-    HIPCHK(c, hipMemcpyAsync(c->sel.p, ident.data(), k * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, h2d(c, c->sel.p, ident.data(), k * 4));
     blsk::launch_pubpoly_eval(c->commits.as<uint32_t>(), c->commit_inf.as<uint8_t>(), (uint32_t)c->t,
                               c->idx.as<uint32_t>(), k, c->pp_tab.as<uint32_t>(), c->pp_inf.as<uint8_t>(), c->stream);
     pk = {c->pp_tab.as<uint32_t>(), c->pp_inf.as<uint8_t>(), c->sel.as<uint32_t>()};
   }
   HIPCHK(c, c->in_sigs.ensure(k * partial_len + 96));
-  HIPCHK(c, hipMemcpyAsync(c->in_sigs.p, partials, k * partial_len, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, h2d(c, c->in_sigs.p, partials, k * partial_len));
   HIPCHK(c, c->bitmap.ensure(((k + 63) / 64) * 8 + 8));
   HIPCHK(c, c->first_bad.ensure(8));
   HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
@@ -662,8 +719,7 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
                   c->first_bad.as<unsigned long long>(), nullptr, c->stream);
     if (rc) return rc;
   }
-  HIPCHK(c, hipMemcpyAsync(cls.data(), c->cls.p, k, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, download_sync(c, {{cls.data(), c->cls.p, k}}));
   return BLSV_OK;
 }
 
@@ -748,15 +804,14 @@ static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std:
   HIPCHK(c, c->lambdas.ensure(t * 32));
   HIPCHK(c, c->scratch.ensure(t * 192 * 4));
   HIPCHK(c, c->out.ensure(96));
-  HIPCHK(c, hipMemcpyAsync(c->sel.p, sel.data(), t * 4, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->idx.p, idx.data(), t * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, h2d(c, c->sel.p, sel.data(), t * 4));
+  HIPCHK(c, h2d(c, c->idx.p, idx.data(), t * 4));
   blsk::launch_lagrange(c->idx.as<uint32_t>(), (uint32_t)t, c->lambdas.as<uint32_t>(), c->stream);
   blsk::launch_lat_recover(c->S.as<uint32_t>(), cls.size(), c->s_inf.as<uint8_t>(), c->sel.as<uint32_t>(),
                            c->lambdas.as<uint32_t>(), (uint32_t)t, c->scratch.as<uint32_t>(), c->out.as<uint8_t>(),
                            c->stream);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(out_sig96, c->out.p, 96, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, download_sync(c, {{out_sig96, c->out.p, 96}}));
   return BLSV_OK;
 }
 

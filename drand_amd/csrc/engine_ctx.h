@@ -178,6 +178,10 @@ struct blsv_ctx {
       pp_tab, pp_inf, sel, g1_cls, misc;
   // one packed upload / download per service batch (svc_verify_mixed)
   PinBuf pin;
+  // pinned staging of the small copies on the main stream (blsverify.cpp h2d / download_sync): uploads
+  // append at io_up_off and wrap after a synchronisation of the stream
+  PinBuf io_up, io_down;
+  size_t io_up_off = 0;
   // speculative recovery beside a round's partial verification (blsverify.cpp spec_recover_*): two
   // slots (V1, V2), each with its decoded shares, Lagrange coefficients, products and output
   struct SpecSlot {

@@ -173,12 +173,11 @@ WVI V mont_reduce(V64 T) {
   V64 ua[4] = {widen(x), vsplat64(0), vsplat64(0), vsplat64(0)};
   sfor<16>([&](auto I) { ua[I & 3] = mad(row_bcast<I>(md), hword(WC_PC0 + I), ua[I & 3]); });
   const V64 u = add64(add64(ua[0], ua[1]), add64(ua[2], ua[3]));  // < 2^56
-  V y = (lo32(u) & M25) + wave_shr1(shr64_lo(u, 25));
-  y = norm1(y);
-  y = norm1(y);  // limbs in [0, 2^25]
+  V y = (lo32(u) & M25) + wave_shr1(shr64_lo(u, 25));  // < 2^25 + 2^31
+  y = norm1(y);  // <= 2^25 + 63: semi-normalized even after the carry below
   // the even row now holds 0 or exactly R: carry one into the odd row's first limb when nonzero. Limbs
-  // up to 2^25 below the top one sum to less than 2^400, so R has a nonzero top limb (lane 15 / 47)
-  // and 0 does not: lanes 16 and 48 test their wave neighbour, no ballot
+  // up to 2^25 + 63 below the top one sum to less than 2^400, so R has a nonzero top limb (lane 15 /
+  // 47) and 0 does not: lanes 16 and 48 test their wave neighbour, no ballot
   const V l = lane_id();
   y = y + sel(((l & 0x1Fu) == 16u) & (wave_shr1(y) != 0u), vsplat(1), vsplat(0));
   return pl16_swap(y, vsplat(0)).b;  // odd rows -> even rows, odd rows zero
