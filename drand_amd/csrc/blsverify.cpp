@@ -287,18 +287,40 @@ static int verify_driver(blsv_ctx* c, size_t n, const uint8_t* d_sigs, size_t st
                          HashFn hash, uint8_t* ok_bitmap, uint64_t* first_bad_idx, uint8_t* reject_class,
                          LatFn lat = LatFn(), bool has_lat = false) {
   const size_t words = (n + 63) / 64;
+  int rc = ensure_workspace(c, n);
+  if (rc) return rc;
+  if (has_lat && use_lat(c, n)) {
+    // the kernel's class bytes come back in one copy and the bitmap and first bad index are read
+    // off them here (launch_finish's rule): no finish kernel, memset or further copies on a call
+    // whose every operation is latency
+    {
+      StageTimer tm(c, ST_LAT, n, c->stream);
+      lat(c->cls.as<uint8_t>());
+    }
+    HIPCHK(c, hipGetLastError());
+    std::vector<uint8_t> own;
+    uint8_t* cls = reject_class;
+    if (!cls) {
+      own.resize(n);
+      cls = own.data();
+    }
+    HIPCHK(c, download_sync(c, {{cls, c->cls.p, n}}));
+    uint64_t fb = UINT64_MAX;
+    for (size_t i = 0; i < n; i++) {
+      if (cls[i] != BLSV_REJ_OK && fb == UINT64_MAX) fb = i;
+      if (ok_bitmap) {
+        if (i % 8 == 0) ok_bitmap[i / 8] = 0;
+        ok_bitmap[i / 8] |= (uint8_t)((cls[i] == BLSV_REJ_OK) << (i % 8));
+      }
+    }
+    if (first_bad_idx) *first_bad_idx = fb;
+    return BLSV_OK;
+  }
   HIPCHK(c, c->bitmap.ensure(words * 8 + 8));
   HIPCHK(c, c->first_bad.ensure(8));
   HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
   if (reject_class) HIPCHK(c, c->misc.ensure(n + 64));
-  int rc = ensure_workspace(c, n);
-  if (rc) return rc;
-  if (has_lat && use_lat(c, n)) {
-    rc = run_lat(c, n, lat, c->bitmap.as<uint64_t>(), c->first_bad.as<unsigned long long>(),
-                 reject_class ? c->misc.as<uint8_t>() : nullptr, c->stream);
-    if (rc) return rc;
-  }
-  for (size_t base = 0; base < n && !(has_lat && use_lat(c, n)); base += c->cap) {
+  for (size_t base = 0; base < n; base += c->cap) {
     const size_t cnt = std::min(c->cap, n - base);
     rc = run_head(c, d_sigs, stride, offset, base, cnt, c->stream, [&]() { hash(base, cnt); });
     if (rc) return rc;
@@ -696,21 +718,18 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
   }
   HIPCHK(c, c->in_sigs.ensure(k * partial_len + 96));
   HIPCHK(c, h2d(c, c->in_sigs.p, partials, k * partial_len));
-  HIPCHK(c, c->bitmap.ensure(((k + 63) / 64) * 8 + 8));
-  HIPCHK(c, c->first_bad.ensure(8));
-  HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
   if (use_lat(c, k)) {
-    // one wave per partial; the decoded sigmas land in S (stride k) for recover_from
-    rc = run_lat(
-        c, k,
-        [&](uint8_t* cls_d) {
-          blsk::launch_lat_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(),
-                                    c->in_sigs.as<uint8_t>(), partial_len, 2, k, pk.tab, pk.inf, pk.idx, cls_d,
-                                    c->S.as<uint32_t>(), c->s_inf.as<uint8_t>(), c->stream);
-        },
-        c->bitmap.as<uint64_t>(), c->first_bad.as<unsigned long long>(), nullptr, c->stream);
-    if (rc) return rc;
+    // one workgroup per partial; the decoded sigmas land in S (stride k) for recover_from. Only the
+    // class bytes are read back (below), so no bitmap pass
+    StageTimer tm(c, ST_LAT, k, c->stream);
+    blsk::launch_lat_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(),
+                              c->in_sigs.as<uint8_t>(), partial_len, 2, k, pk.tab, pk.inf, pk.idx, c->cls.as<uint8_t>(),
+                              c->S.as<uint32_t>(), c->s_inf.as<uint8_t>(), c->stream);
+    HIPCHK(c, hipGetLastError());
   } else {
+    HIPCHK(c, c->bitmap.ensure(((k + 63) / 64) * 8 + 8));
+    HIPCHK(c, c->first_bad.ensure(8));
+    HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
     blsk::launch_hash_messages(c->in_msgs.as<uint8_t>(), c->in_off.as<uint64_t>(), c->in_len.as<uint32_t>(), k,
                                c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(), c->HQ.as<uint32_t>(), c->stream);
     rc = run_head(c, c->in_sigs.as<uint8_t>(), partial_len, 2, 0, k, c->stream, []() {});  // hashed above

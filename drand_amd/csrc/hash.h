@@ -54,6 +54,73 @@ DI void sha256_compress(uint32_t (&st)[8], const uint32_t (&blk)[16]) {
   st[7] += h;
 }
 
+// The same compression as straight VALU code for the latency engine's wave-uniform hashing (one
+// wave runs ~20 compressions in a row on a lone verify's critical path): every rotation one
+// v_alignbit, Ch and Maj one v_bfi_b32 each, the three-way xor of Sigma0/Sigma1 folded into the add
+// that consumes it (v_xad_u32: (a ^ b) + c) -- 17 operations per round and 11 per schedule word
+// against ~28 and ~14 from the plain form, whose uniform data the compiler otherwise keeps on the
+// scalar unit with a lane read-back per rotation.
+#ifdef BLS_HOST
+DI void sha256_compress_fast(uint32_t (&st)[8], const uint32_t (&blk)[16]) { sha256_compress(st, blk); }
+#else
+DI uint32_t v_bfi(uint32_t m, uint32_t a, uint32_t b) {  // (m & a) | (~m & b)
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+DI uint32_t v_xad(uint32_t a, uint32_t b, uint32_t c) {  // (a ^ b) + c
+  uint32_t r;
+  asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+DI uint32_t v_ror(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+DI void sha256_compress_fast(uint32_t (&st)[8], const uint32_t (&blk)[16]) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) w[i] = blk[i];
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int t = 0; t < 64; t++) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      const uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+      const uint32_t s0 = v_xad(v_ror(w15, 7) ^ v_ror(w15, 18), w15 >> 3, w[t & 15]);  // sigma0 + w[t-16]
+      const uint32_t s1 = v_xad(v_ror(w2, 17) ^ v_ror(w2, 19), w2 >> 10, w[(t - 7) & 15]);
+      wt = s0 + s1;
+      w[t & 15] = wt;
+    }
+    const uint32_t t1 = v_xad(v_ror(e, 6) ^ v_ror(e, 11), v_ror(e, 25), v_bfi(e, f, g)) + h + wt + SHA256_K[t];
+    const uint32_t t2 = v_xad(v_ror(a, 2) ^ v_ror(a, 13), v_ror(a, 22), v_bfi(a ^ b, c, b));  // Sigma0 + Maj
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  st[0] += a;
+  st[1] += b;
+  st[2] += c;
+  st[3] += d;
+  st[4] += e;
+  st[5] += f;
+  st[6] += g;
+  st[7] += h;
+}
+#endif
+
+// the batch kernels' choice (k_hash.hip): the plain form unless built with BLS_SHA_FAST_BATCH=1
+#ifndef BLS_SHA_FAST_BATCH
+#define BLS_SHA_FAST_BATCH 0
+#endif
+DI void sha256_compress_batch(uint32_t (&st)[8], const uint32_t (&blk)[16]) {
+  if constexpr (BLS_SHA_FAST_BATCH) sha256_compress_fast(st, blk); else sha256_compress(st, blk);
+}
+
 DI void sha256_init(uint32_t (&st)[8]) {
 #pragma unroll
   for (int i = 0; i < 8; i++) st[i] = SHA256_IV[i];
@@ -65,7 +132,11 @@ DI uint32_t load_be32(const uint8_t* p) {
 
 // chain.Message(round, prev) for prev of 96 bytes (104-byte message, 2 blocks) or 32 bytes
 // (40-byte message, 1 block: the round-1 genesis seed, chain/store.go:46-51, client/verify.go:122).
+template <bool FAST = false>
 DI void drand_message(uint32_t (&out)[8], const uint8_t* prev, int prev_len, uint64_t round) {
+  auto compress = [](uint32_t(&s_)[8], const uint32_t(&b_)[16]) {
+    if constexpr (FAST) sha256_compress_fast(s_, b_); else sha256_compress(s_, b_);
+  };
   uint32_t st[8];
   sha256_init(st);
   uint32_t blk[16];
@@ -73,7 +144,7 @@ DI void drand_message(uint32_t (&out)[8], const uint8_t* prev, int prev_len, uin
   if (prev_len == 96) {
 #pragma unroll
     for (int i = 0; i < 16; i++) blk[i] = load_be32(prev + 4 * i);
-    sha256_compress(st, blk);
+    compress(st, blk);
 #pragma unroll
     for (int i = 0; i < 8; i++) blk[i] = load_be32(prev + 64 + 4 * i);
     blk[8] = rhi;
@@ -82,7 +153,7 @@ DI void drand_message(uint32_t (&out)[8], const uint8_t* prev, int prev_len, uin
 #pragma unroll
     for (int i = 11; i < 15; i++) blk[i] = 0;
     blk[15] = 104 * 8;
-    sha256_compress(st, blk);
+    compress(st, blk);
   } else {  // 32-byte prev
 #pragma unroll
     for (int i = 0; i < 8; i++) blk[i] = load_be32(prev + 4 * i);
@@ -92,14 +163,18 @@ DI void drand_message(uint32_t (&out)[8], const uint8_t* prev, int prev_len, uin
 #pragma unroll
     for (int i = 11; i < 15; i++) blk[i] = 0;
     blk[15] = 40 * 8;
-    sha256_compress(st, blk);
+    compress(st, blk);
   }
 #pragma unroll
   for (int i = 0; i < 8; i++) out[i] = st[i];
 }
 
 // chain.MessageV2(round)
+template <bool FAST = false>
 DI void drand_message_v2(uint32_t (&out)[8], uint64_t round) {
+  auto compress = [](uint32_t(&s_)[8], const uint32_t(&b_)[16]) {
+    if constexpr (FAST) sha256_compress_fast(s_, b_); else sha256_compress(s_, b_);
+  };
   uint32_t st[8];
   sha256_init(st);
   uint32_t blk[16];
@@ -109,7 +184,7 @@ DI void drand_message_v2(uint32_t (&out)[8], uint64_t round) {
 #pragma unroll
   for (int i = 3; i < 15; i++) blk[i] = 0;
   blk[15] = 64;
-  sha256_compress(st, blk);
+  compress(st, blk);
 #pragma unroll
   for (int i = 0; i < 8; i++) out[i] = st[i];
 }
@@ -143,8 +218,8 @@ DI void xmd_tail_to_field(const uint32_t (&b0)[8], fp2& u0, fp2& u1) {
       blk[8 + i] = XMD_BI_A_TAIL[i];
     }
     blk[8] |= (uint32_t)k << 24;
-    sha256_compress(st, blk);
-    sha256_compress(st, XMD_BI_B);
+    sha256_compress_batch(st, blk);
+    sha256_compress_batch(st, XMD_BI_B);
     if (k & 1) {
 #pragma unroll
       for (int i = 0; i < 8; i++) prev[i] = st[i];
@@ -165,7 +240,11 @@ DI void xmd_tail_to_field(const uint32_t (&b0)[8], fp2& u0, fp2& u1) {
 
 // b_0 of expand_message_xmd for an arbitrary-length message (bytes), DST bytes from dst_rt
 // (a runtime-indexable copy of DST): Z_pad || msg || 01 00 || 00 || DST || 2b
+template <bool FAST = false>
 DI void xmd_b0_bytes(uint32_t (&b0)[8], const uint8_t* msg, uint32_t len, const uint8_t* dst_rt) {
+  auto compress = [](uint32_t(&s_)[8], const uint32_t(&b_)[16]) {
+    if constexpr (FAST) sha256_compress_fast(s_, b_); else sha256_compress(s_, b_);
+  };
   uint32_t st[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) st[i] = SHA256_ZPAD_MIDSTATE[i];
@@ -194,7 +273,7 @@ DI void xmd_b0_bytes(uint32_t (&b0)[8], const uint8_t* msg, uint32_t len, const 
       blk[14] = (uint32_t)(total_bits >> 32);
       blk[15] = (uint32_t)total_bits;
     }
-    sha256_compress(st, blk);
+    compress(st, blk);
   }
 #pragma unroll
   for (int i = 0; i < 8; i++) b0[i] = st[i];
@@ -213,8 +292,8 @@ DI void hash_to_field_fp2(const uint32_t (&msg)[8], fp2& u0, fp2& u1) {
       blk[i] = msg[i];
       blk[8 + i] = XMD_B0_A_TAIL[i];
     }
-    sha256_compress(st, blk);
-    sha256_compress(st, XMD_B0_B);
+    sha256_compress_batch(st, blk);
+    sha256_compress_batch(st, XMD_B0_B);
 #pragma unroll
     for (int i = 0; i < 8; i++) b0[i] = st[i];
   }

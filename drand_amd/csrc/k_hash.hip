@@ -91,7 +91,7 @@ BLS_KERNEL(BLS_WPE_HASH_A) k_hash_chained(ChainedSrc src, size_t base, size_t cn
     prev_len = 96;
   }
   uint32_t msg[8];
-  drand_message(msg, prev, prev_len, src.first_round + g);
+  drand_message<BLS_SHA_FAST_BATCH>(msg, prev, prev_len, src.first_round + g);
   fp2 u0, u1;
   hash_to_field_fp2(msg, u0, u1);
   hash_a_store<SPLIT>(u0, u1, k, Q, cnt, i);
@@ -106,7 +106,7 @@ BLS_KERNEL(BLS_WPE_HASH_A) k_hash_unchained(const uint64_t* rounds, uint64_t fir
   if (i >= cnt) return;
   const uint64_t round = rounds ? rounds[base + i] : first_round + base + i;
   uint32_t msg[8];
-  drand_message_v2(msg, round);
+  drand_message_v2<BLS_SHA_FAST_BATCH>(msg, round);
   fp2 u0, u1;
   hash_to_field_fp2(msg, u0, u1);
   hash_a_store<SPLIT>(u0, u1, k, Q, cnt, i);
@@ -120,7 +120,7 @@ BLS_KERNEL(BLS_WPE_HASH_A) k_hash_messages(const uint8_t* msgs, const uint64_t* 
   hash_a_index<SPLIT>(k, i);
   if (i >= cnt) return;
   uint32_t b0[8];
-  xmd_b0_bytes(b0, msgs + off[i], len[i], c_dst);
+  xmd_b0_bytes<BLS_SHA_FAST_BATCH>(b0, msgs + off[i], len[i], c_dst);
   fp2 u0, u1;
   xmd_tail_to_field(b0, u0, u1);
   hash_a_store<SPLIT>(u0, u1, k, Q, cnt, i);

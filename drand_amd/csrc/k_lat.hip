@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(64 * WV_WAVES) k_lat_chained(ChainedSrc src, s
         const uint8_t* prev = seg_start ? src.seeds + seg * 96 : src.sigs + (g - 1) * 96;
         const int prev_len = seg_start ? (seg == 0 ? (int)src.seed0_len : 96) : 96;
         uint32_t msg[8];
-        drand_message(msg, prev, prev_len, src.first_round + g);
+        drand_message<true>(msg, prev, prev_len, src.first_round + g);
         wv::xmd_b0_msg32(msg, b0);
       },
       i, src.sigs + g * 96, pk_tab, pk_inf, nullptr, cls, nullptr, nullptr, 0);
@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(64 * WV_WAVES) k_lat_unchained(const uint64_t*
   lat_verify(
       [&](uint32_t(&b0)[8]) {
         uint32_t msg[8];
-        drand_message_v2(msg, rounds ? rounds[base + i] : first_round + base + i);
+        drand_message_v2<true>(msg, rounds ? rounds[base + i] : first_round + base + i);
         wv::xmd_b0_msg32(msg, b0);
       },
       i, sigs + (base + i) * 96, pk_tab, pk_inf, nullptr, cls, nullptr, nullptr, 0);
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(64 * WV_WAVES) k_lat_messages(const uint8_t* m
                                                      uint8_t* s_inf) {
   const size_t i = blockIdx.x;
   if (i >= cnt) return;
-  lat_verify([&](uint32_t(&b0)[8]) { xmd_b0_bytes(b0, msgs + off[i], len[i], c_lat_dst); }, i,
+  lat_verify([&](uint32_t(&b0)[8]) { xmd_b0_bytes<true>(b0, msgs + off[i], len[i], c_lat_dst); }, i,
              sigs + i * stride + offset, pk_tab, pk_inf, pk_idx, cls, S, s_inf, cnt);
 }
 

@@ -276,14 +276,17 @@ WV_NOINL V dot6_v(V a0, V b0, V a1, V b1, V a2, V b2, V a3, V b3, V a4, V b4, V 
   return dot_body<6>(a, b);
 }
 // pair product [a0 b0 | a1 b1]
-WV_NOINL V mulp_v(V a, V b) {
-  WV_COUNT(OPC_MULP);
+WVI V mulp_body(V a, V b) {
   stage_term(0, a, b);
   wsync();
   V64 s[4] = {vsplat64(0), vsplat64(0), vsplat64(0), vsplat64(0)};
   acc_pair(0, s);
   wsync();
   return mont_reduce(sum4(s));
+}
+WV_NOINL V mulp_v(V a, V b) {
+  WV_COUNT(OPC_MULP);
+  return mulp_body(a, b);
 }
 // Fp2 square [(a0 + a1)(a0 + D - a1) | (2 a0) a1] as one pair product
 WV_NOINL V sqr2_v(V a) {
@@ -356,6 +359,14 @@ WVI F mulp(const F& a, const F& b) {
 // (a pair square with each cross product once -- 9 products per lane against 16, lane-dependent LDS
 // addresses -- measured 0.75 us against the general product's 0.69, profiles/r04zb_wvbench.json)
 WVI F sqrp(const F& a) { return mulp(a, a); }
+// the same square with its body inlined at the call site: for the long squaring chains (wvteam.h
+// ring_pow_produce), where a call's entry wait for every outstanding LDS operation (the ring's stores
+// and posts) and its argument moves sit on the critical path 378 times per exponentiation
+WVI F sqrp_inl(const F& a) {
+  WV_REQUIRE(bnd(a), OPND_MAX, "sqrp a");
+  WV_COUNT(OPC_MULP);
+  return mkF(mulp_body(a.x, a.x), bnd(a) * bnd(a) * P_OVER_R + RED_SLACK);
+}
 WVI F sqr2(const F& a) {
   WV_REQUIRE(bnd(a), DMUL_BMAX, "sqr2");
   return mkF(sqr2_v(a.x), 2 * bnd(a) * (bnd(a) + DMUL_M) * P_OVER_R + RED_SLACK);

@@ -59,8 +59,8 @@ WVI void xmd_b0_msg32(const uint32_t (&msg)[8], uint32_t (&b0)[8]) {
     blk[i] = msg[i];
     blk[8 + i] = bls::XMD_B0_A_TAIL[i];
   }
-  bls::sha256_compress(st, blk);
-  bls::sha256_compress(st, bls::XMD_B0_B);
+  bls::sha256_compress_fast(st, blk);
+  bls::sha256_compress_fast(st, bls::XMD_B0_B);
   for (int i = 0; i < 8; i++) b0[i] = st[i];
 }
 
@@ -76,8 +76,8 @@ WVI void xmd_words(const uint32_t (&b0)[8], uint32_t (&e)[4][16]) {
       blk[8 + i] = bls::XMD_BI_A_TAIL[i];
     }
     blk[8] |= (uint32_t)k << 24;
-    bls::sha256_compress(st, blk);
-    bls::sha256_compress(st, bls::XMD_BI_B);
+    bls::sha256_compress_fast(st, blk);
+    bls::sha256_compress_fast(st, bls::XMD_BI_B);
     for (int i = 0; i < 8; i++) {
       e[(k - 1) / 2][((k - 1) & 1) * 8 + i] = st[i];
       prev[i] = st[i];

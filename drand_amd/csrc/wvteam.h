@@ -139,7 +139,7 @@ WVI F ring_pow_produce(const Ring& rg, const F& a, const uint32_t (&e)[NW], Ring
       flag_post_lds(rg.ctr0);
       rc.produced++;
     }
-    if (i + 1 < nb) x = sqrp(x);
+    if (i + 1 < nb) x = sqrp_inl(x);
   }
   rc.results++;
   flag_wait(rg.ctr0 + 2, rc.results);
