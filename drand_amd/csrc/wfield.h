@@ -67,8 +67,19 @@ constexpr int MAX_TERMS = 6;
 // wv_init, in table order WC_PC0.., so a product reads them at LDS latency instead of a global load's
 constexpr int HOT_FIRST = WC_DSUB0;  // DSUB0, DSUB1, DSUB2, DMUL, PC0..PC15 are consecutive
 constexpr int HOT_COUNT = WC_PC15 + 1 - WC_DSUB0;
-constexpr int LDS_WORDS = SLOT_WORDS * MAX_TERMS + 64 * HOT_COUNT;
+// the table constants the team rounds read (the cyclotomic square's +-2, the curve formulas' -1, -2, -8,
+// one, and p for the canonical forms): also per-wave LDS copies, read at LDS latency instead of a
+// global load's in every round
+constexpr int HOT2_IDS[] = {WC_ONE2, WC_NEG2, WC_NEG1, WC_POS2, WC_NEG8, WC_ONE_DUP, WC_P_DUP};
+constexpr int HOT2_COUNT = sizeof(HOT2_IDS) / sizeof(HOT2_IDS[0]);
+constexpr int hot2_index(int id) {
+  for (int i = 0; i < HOT2_COUNT; i++)
+    if (HOT2_IDS[i] == id) return i;
+  return -1;
+}
+constexpr int LDS_WORDS = SLOT_WORDS * MAX_TERMS + 64 * HOT_COUNT + 64 * HOT2_COUNT;
 constexpr int L_HOT = SLOT_WORDS * MAX_TERMS;
+constexpr int L_HOT2 = L_HOT + 64 * HOT_COUNT;
 constexpr int L_WIN = 0, L_BX = 96, L_BZ = 160;
 
 #ifdef WV_HOST
@@ -124,7 +135,11 @@ WVI uint32_t* wave_lds() { return g_wv_lds + (threadIdx.x >> 6) * LDS_WORDS; }
 
 // ------------------------------------------------------------------ lane geometry and constants
 WVI M in_half0() { return lane_id() < 32u; }
-WVI V cword(int id) { return gld(WV_CONST_TABLE + id * 64, lane_id()); }
+WVI V cword(int id) {
+  const int h = hot2_index(id);  // a compile-time constant at every call with a literal id
+  if (h >= 0) return lds_ld(wave_lds() + L_HOT2 + h * 64, lane_id());
+  return gld(WV_CONST_TABLE + id * 64, lane_id());
+}
 // a hot constant (HOT_FIRST <= id < HOT_FIRST + HOT_COUNT) from the wave's LDS copy
 WVI V hword(int id) { return lds_ld(wave_lds() + L_HOT + (id - HOT_FIRST) * 64, lane_id()); }
 WVI F cst(int id) { return mkF(cword(id), 1.0); }  // every table constant used as a value is < p
@@ -136,6 +151,7 @@ WVI void wv_init() {
   const V off = (l >> 5) * 48u + (l & 15u);  // words h*48 + 0..15 (odd-row lanes repeat them)
   for (int s = 0; s < MAX_TERMS; s++) lds_st(lds + s * SLOT_WORDS, off, vsplat(0));
   for (int c = 0; c < HOT_COUNT; c++) lds_st(lds + L_HOT + c * 64, l, cword(HOT_FIRST + c));
+  for (int c = 0; c < HOT2_COUNT; c++) lds_st(lds + L_HOT2 + c * 64, l, gld(WV_CONST_TABLE + HOT2_IDS[c] * 64, l));
 }
 
 // LDS hand-off: a wave's ds instructions execute in order; this keeps the compiler from moving a
