@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--lat-max", type=int, default=None,
                     help="latency-path cutover for this run (0 = batch pipeline only; default: the library's)")
     ap.add_argument("--sweep", default="", help="batch sizes for the latency-vs-batch crossover")
+    ap.add_argument("--agg-only", type=int, default=0,
+                    help="run only the aggregator round this many times (under rocprofv3 --kernel-trace)")
     a = ap.parse_args()
     from drand_amd.engine import Engine
 
@@ -74,6 +76,13 @@ def main():
         eng.set_lat_max(cur)
         out["lat_max"] = cur
         eng.set_public_key(bytes.fromhex(ch["pk"]))
+        if a.agg_only:
+            eng.set_group(commits, th["n"])
+            for _ in range(a.agg_only):
+                ok, _, sig, gok = eng.aggregate(msg, partials, th["t"], th["n"])
+                assert all(ok) and gok and sig.hex() == th["group_sig"]
+            print("aggregate rounds:", a.agg_only)
+            return
 
         def lone_beacon():
             r = eng.verify_chained(2, sigs[0], [sigs[1]])
