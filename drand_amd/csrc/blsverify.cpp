@@ -440,6 +440,8 @@ int blsv_create(int device, blsv_ctx** out) {
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->spec_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -454,11 +456,12 @@ int blsv_create(int device, blsv_ctx** out) {
 void blsv_destroy(blsv_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  for (hipStream_t s : {c->stream, c->side}) {
+  for (hipStream_t s : {c->stream, c->side, c->side2}) {
     if (!s) continue;
     (void)hipStreamSynchronize(s);
     (void)hipStreamDestroy(s);
   }
+  if (c->spec_ev) (void)hipEventDestroy(c->spec_ev);
   if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
   if (c->join_ev) (void)hipEventDestroy(c->join_ev);
   (void)hipDeviceSynchronize();
@@ -857,7 +860,10 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
   auto& sp = c->spec[slot];
   const size_t tt = sr.sel.size();
   const size_t host_need = tt * 96 + tt * 4 + tt * 4 + 128;
-  if (sp.host.sz < host_need) HIPCHK(c, hipStreamSynchronize(c->side));  // no copy may be pending on it
+  if (sp.host.sz < host_need) {  // no copy may be pending on it
+    HIPCHK(c, hipStreamSynchronize(c->side));
+    HIPCHK(c, hipStreamSynchronize(c->side2));
+  }
   HIPCHK(c, sp.host.ensure(host_need));
   uint8_t* h_sig = sp.host.as<uint8_t>();
   uint32_t* h_idx = reinterpret_cast<uint32_t*>(h_sig + tt * 96);
@@ -876,13 +882,17 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
   HIPCHK(c, sp.lam.ensure(tt * 32));
   HIPCHK(c, sp.scratch.ensure(tt * 192 * 4));
   HIPCHK(c, sp.out.ensure(96));
+  // the Lagrange coefficients (indices only) on the second side stream beside the decoding; the
+  // interpolation waits for both
   hipStream_t st = c->side;
+  HIPCHK(c, hipMemcpyAsync(sp.idx.p, h_idx, tt * 4, hipMemcpyHostToDevice, c->side2));
+  blsk::launch_lagrange(sp.idx.as<uint32_t>(), (uint32_t)tt, sp.lam.as<uint32_t>(), c->side2);
+  HIPCHK(c, hipEventRecord(c->spec_ev, c->side2));
   HIPCHK(c, hipMemcpyAsync(sp.sig.p, h_sig, tt * 96, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(sp.idx.p, h_idx, tt * 4, hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpyAsync(sp.sel.p, h_sel, tt * 4, hipMemcpyHostToDevice, st));
-  blsk::launch_decompress_g2_only(sp.sig.as<uint8_t>(), 96, 0, tt, sp.S.as<uint32_t>(), sp.s_inf.as<uint8_t>(),
-                                  sp.cls.as<uint8_t>(), st);
-  blsk::launch_lagrange(sp.idx.as<uint32_t>(), (uint32_t)tt, sp.lam.as<uint32_t>(), st);
+  blsk::launch_lat_decode(sp.sig.as<uint8_t>(), 96, 0, tt, sp.S.as<uint32_t>(), sp.s_inf.as<uint8_t>(),
+                          sp.cls.as<uint8_t>(), st);
+  HIPCHK(c, hipStreamWaitEvent(st, c->spec_ev, 0));
   blsk::launch_lat_recover(sp.S.as<uint32_t>(), tt, sp.s_inf.as<uint8_t>(), sp.sel.as<uint32_t>(),
                            sp.lam.as<uint32_t>(), (uint32_t)tt, sp.scratch.as<uint32_t>(), sp.out.as<uint8_t>(), st);
   HIPCHK(c, hipGetLastError());

@@ -154,6 +154,10 @@ struct blsv_ctx {
   // joined back into the launch stream with these two events
   hipStream_t side = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  // the speculative recovery's Lagrange coefficients beside its decoding (blsverify.cpp
+  // spec_recover_launch): a second side stream, joined into `side` through spec_ev
+  hipStream_t side2 = nullptr;
+  hipEvent_t spec_ev = nullptr;
   std::string err;
   // group
   bool has_group = false;

@@ -98,6 +98,40 @@ __global__ void __launch_bounds__(64 * WV_WAVES) k_lat_messages(const uint8_t* m
              sigs + i * stride + offset, pk_tab, pk_inf, pk_idx, cls, S, s_inf, cnt);
 }
 
+// decode only (the speculative recovery's shares, blsverify.cpp spec_recover_launch): one workgroup of
+// two waves per signature, wave 0 decoding (whash.h g2_decompress, no subgroup check: validity is the
+// partials' verdict) while wave 1 multiplies for its two square roots, as the signature branch of
+// wvteam.h verify_team does; sigma lands in S (stride cnt) as k_lat_messages stores it. Replaces the
+// one-lane-per-item batch decompression there, whose serial chains took ~1.3 ms for a lone item.
+__global__ void __launch_bounds__(64 * WV_WAVES) k_lat_decode(const uint8_t* sigs, size_t stride, size_t offset,
+                                                             size_t cnt, uint32_t* S, uint8_t* s_inf, uint8_t* cls) {
+  const size_t i = blockIdx.x;
+  if (i >= cnt) return;
+  wv::team_init();
+  wv::wv_init();
+  __syncthreads();
+  const int w = wv::wave_id();
+  wv::RingCounts rc;
+  if (w == 0) {
+    wv::F x, y;
+    bool inf = false;
+    const uint8_t c = wv::g2_decompress(sigs + i * stride + offset, x, y, inf, false,
+                                        wv::PowRing{&wv::SIG_RING, &rc});
+    wv::flag_post(wv::CTR_DEC);  // stops the multiplier when the decode rejected before a root
+    if (threadIdx.x == 0) cls[i] = c;
+    store_sigma(S, s_inf, cnt, i, x, y, c != REJ_OK || inf);
+  } else if (w == 1) {
+    for (int k = 0; k < wv::DEC_POWS; k++)
+      if (!wv::ring_pow_consume(wv::SIG_RING, bls::EXP_P_MINUS_3_DIV_4, rc, wv::CTR_DEC)) break;
+  }
+}
+
+void launch_lat_decode(const uint8_t* sigs, size_t stride, size_t offset, size_t cnt, uint32_t* S, uint8_t* s_inf,
+                       uint8_t* cls, hipStream_t st) {
+  if (!cnt) return;
+  hipLaunchKernelGGL(k_lat_decode, dim3((unsigned)cnt), dim3(128), 0, st, sigs, stride, offset, cnt, S, s_inf, cls);
+}
+
 // the phase marks of the last latency launch's item 0 (wteam.h WV_MARK), device wall-clock ticks
 int lat_trace_read(uint64_t* out, int n, hipStream_t st) {
   if (n > wv::LAT_TRACE_N) n = wv::LAT_TRACE_N;

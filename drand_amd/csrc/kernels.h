@@ -86,6 +86,9 @@ void launch_decompress_g1(const uint8_t* in, size_t cnt, uint32_t* tab, uint8_t*
 void launch_pubpoly_eval(const uint32_t* commits, const uint8_t* commit_inf, uint32_t t, const uint32_t* idx,
                          size_t cnt, uint32_t* out_tab, uint8_t* out_inf, hipStream_t st);
 // Lagrange basis at 0 for x_i = idx[i] + 1 over Fr, written as plain 8-word little-endian scalars
+// decode only on the latency engine (k_lat.hip; one two-wave workgroup per signature)
+void launch_lat_decode(const uint8_t* sigs, size_t stride, size_t offset, size_t cnt, uint32_t* S, uint8_t* s_inf,
+                       uint8_t* cls, hipStream_t st);
 void launch_decompress_g2_only(const uint8_t* sigs, size_t stride, size_t offset, size_t cnt, uint32_t* S,
                                uint8_t* s_inf, uint8_t* cls, hipStream_t st);
 void launch_lagrange(const uint32_t* idx, uint32_t t, uint32_t* lambdas, hipStream_t st);
