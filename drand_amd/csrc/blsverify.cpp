@@ -847,19 +847,24 @@ static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std:
 // path, whose partial verification leaves the side stream idle.
 struct SpecRecover {
   bool launched = false;
+  bool verified = false;      // VerifyRecovered of the speculative signature queued behind it too
   std::vector<uint32_t> sel;  // round positions of the shares used
 };
 
 static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, size_t partial_len,
                                const std::vector<uint32_t>& index, size_t lo, size_t hi, size_t t, size_t n,
-                               SpecRecover& sr) {
+                               SpecRecover& sr, const uint8_t* vmsg = nullptr, size_t vmsg_len = 0) {
   sr.launched = false;
+  sr.verified = false;
   std::vector<uint8_t> all_ok(index.size(), BLSV_REJ_OK);
   std::vector<uint32_t> idx;
   if (!select_shares(all_ok, index, lo, hi, t, n, sr.sel, idx)) return BLSV_OK;  // recover_from will say so
   auto& sp = c->spec[slot];
   const size_t tt = sr.sel.size();
-  const size_t host_need = tt * 96 + tt * 4 + tt * 4 + 128;
+  // host staging: sigmas | indices | selection | 96-byte result | verify class | message, offsets, length
+  const size_t v_off = tt * 96 + tt * 8 + 96, m_off = v_off + 64;
+  const bool verify = vmsg != nullptr && vmsg_len <= kIoCap / 4;
+  const size_t host_need = m_off + (verify ? vmsg_len + 64 : 0) + 64;
   if (sp.host.sz < host_need) {  // no copy may be pending on it
     HIPCHK(c, hipStreamSynchronize(c->side));
     HIPCHK(c, hipStreamSynchronize(c->side2));
@@ -897,6 +902,31 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
                            sp.lam.as<uint32_t>(), (uint32_t)tt, sp.scratch.as<uint32_t>(), sp.out.as<uint8_t>(), st);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(h_sig + tt * 96 + tt * 8, sp.out.p, 96, hipMemcpyDeviceToHost, st));
+  if (verify) {
+    // VerifyRecovered(group key, msg, speculative signature) right behind the recovery on the side
+    // stream: the same latency kernel verify_messages would launch for it (kept on a hit)
+    uint8_t* h_msg = h_sig + m_off;
+    std::memcpy(h_msg, vmsg, vmsg_len);
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(h_msg + ((vmsg_len + 7) & ~size_t(7)));
+    h_off[0] = 0;
+    h_off[1] = vmsg_len;
+    uint32_t* h_len = reinterpret_cast<uint32_t*>(h_off + 2);
+    h_len[0] = (uint32_t)vmsg_len;
+    HIPCHK(c, sp.vmsg.ensure(vmsg_len + 1));
+    HIPCHK(c, sp.voff.ensure(16));
+    HIPCHK(c, sp.vlen.ensure(4));
+    HIPCHK(c, sp.vcls.ensure(64));
+    if (vmsg_len) HIPCHK(c, hipMemcpyAsync(sp.vmsg.p, h_msg, vmsg_len, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(sp.voff.p, h_off, 16, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(sp.vlen.p, h_len, 4, hipMemcpyHostToDevice, st));
+    const PkSel pk = group_pk(c);
+    blsk::launch_lat_messages(sp.vmsg.as<uint8_t>(), sp.voff.as<uint64_t>(), sp.vlen.as<uint32_t>(),
+                              sp.out.as<uint8_t>(), 96, 0, 1, pk.tab, pk.inf, pk.idx, sp.vcls.as<uint8_t>(), nullptr,
+                              nullptr, st);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(h_sig + v_off, sp.vcls.p, 1, hipMemcpyDeviceToHost, st));
+    sr.verified = true;
+  }
   sr.launched = true;
   return BLSV_OK;
 }
@@ -905,13 +935,16 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
 // recover_from; the side stream is drained either way
 static int spec_recover_finish(blsv_ctx* c, int slot, const SpecRecover& sr, const std::vector<uint8_t>& cls,
                                const std::vector<uint32_t>& index, size_t lo, size_t hi, size_t t, size_t n,
-                               uint8_t* out_sig96) {
+                               uint8_t* out_sig96, int* vcls = nullptr) {
+  if (vcls) *vcls = -1;  // no speculative VerifyRecovered verdict
   if (sr.launched) {
     HIPCHK(c, hipStreamSynchronize(c->side));
     std::vector<uint32_t> sel, idx;
     if (select_shares(cls, index, lo, hi, t, n, sel, idx) && sel == sr.sel) {
       const size_t tt = sr.sel.size();
-      std::memcpy(out_sig96, c->spec[slot].host.as<uint8_t>() + tt * 96 + tt * 8, 96);
+      const uint8_t* h = c->spec[slot].host.as<uint8_t>();
+      std::memcpy(out_sig96, h + tt * 96 + tt * 8, 96);
+      if (vcls && sr.verified) *vcls = h[tt * 96 + tt * 8 + 96];
       c->spec_hits++;
       return BLSV_OK;
     }
@@ -942,7 +975,7 @@ int blsv_aggregate(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_
   SpecRecover sr;
   if (spec_applies(c, k, partial_len)) {
     share_indices(partials, partial_len, k, index);
-    int rc0 = spec_recover_launch(c, 0, partials, partial_len, index, 0, k, t, n, sr);
+    int rc0 = spec_recover_launch(c, 0, partials, partial_len, index, 0, k, t, n, sr, msg, msg_len);
     if (rc0) return rc0;
   }
   int rc = partials_stage(c, msg, msg_len, partials, partial_len, k, cls, index);
@@ -955,8 +988,13 @@ int blsv_aggregate(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_
     if (reject_class) reject_class[i] = cls[i];
   }
   *group_ok = 0;
-  rc = spec_recover_finish(c, 0, sr, cls, index, 0, k, t, n, out_sig96);
+  int vcls = -1;
+  rc = spec_recover_finish(c, 0, sr, cls, index, 0, k, t, n, out_sig96, &vcls);
   if (rc) return rc;
+  if (vcls >= 0) {  // the speculative VerifyRecovered of this very signature
+    *group_ok = vcls == BLSV_REJ_OK;
+    return BLSV_OK;
+  }
   // VerifyRecovered(group key, msg, sig) (chain/beacon/chain.go:141)
   const uint32_t len = (uint32_t)msg_len;
   uint8_t bm = 0, cls1 = 0;
@@ -1000,8 +1038,10 @@ int blsv_aggregate_round(blsv_ctx* c, const uint8_t* msg1, size_t msg1_len, cons
   SpecRecover sr1, sr2;  // both recoveries speculated on the side stream (see spec_recover_launch)
   if (spec_applies(c, k, partial_len)) {
     share_indices(parts.data(), partial_len, k, index);
-    int rc0 = spec_recover_launch(c, 0, parts.data(), partial_len, index, 0, k1, t, n, sr1);
-    if (!rc0 && try_v2) rc0 = spec_recover_launch(c, 1, parts.data(), partial_len, index, k1, k, t, n, sr2);
+    int rc0 = spec_recover_launch(c, 0, parts.data(), partial_len, index, 0, k1, t, n, sr1, msg1 ? msg1 : parts.data(),
+                                  msg1_len);
+    if (!rc0 && try_v2)
+      rc0 = spec_recover_launch(c, 1, parts.data(), partial_len, index, k1, k, t, n, sr2, msg2, msg2_len);
     if (rc0) {
       (void)hipStreamSynchronize(c->side);
       return rc0;
@@ -1015,7 +1055,8 @@ int blsv_aggregate_round(blsv_ctx* c, const uint8_t* msg1, size_t msg1_len, cons
   for (size_t i = 0; i < k1; i++) ok1[i] = cls[i] == BLSV_REJ_OK;
   for (size_t i = 0; i < k2; i++) ok2[i] = cls[k1 + i] == BLSV_REJ_OK;
   // Recover V1 (chain.go:136) and, with LenV2 >= thr, V2 (chain.go:153-155) from the staged shares
-  rc = spec_recover_finish(c, 0, sr1, cls, index, 0, k1, t, n, sig1_96);
+  int vc1 = -1, vc2 = -1;
+  rc = spec_recover_finish(c, 0, sr1, cls, index, 0, k1, t, n, sig1_96, &vc1);
   if (rc == BLSV_ENOTENOUGH) {
     if (sr2.launched) (void)hipStreamSynchronize(c->side);
     return BLSV_OK;  // "invalid_recovery": no beacon this time
@@ -1023,7 +1064,7 @@ int blsv_aggregate_round(blsv_ctx* c, const uint8_t* msg1, size_t msg1_len, cons
   if (rc) return rc;
   bool v2_recovered = false;
   if (try_v2) {
-    rc = spec_recover_finish(c, 1, sr2, cls, index, k1, k, t, n, sig2_96);
+    rc = spec_recover_finish(c, 1, sr2, cls, index, k1, k, t, n, sig2_96, &vc2);
     if (rc && rc != BLSV_ENOTENOUGH) return rc;
     v2_recovered = rc == BLSV_OK;
   }
@@ -1036,8 +1077,12 @@ int blsv_aggregate_round(blsv_ctx* c, const uint8_t* msg1, size_t msg1_len, cons
   }
   uint8_t bm = 0, vcls[2] = {0, 0};
   uint64_t fb = 0;
-  rc = blsv_verify_messages(c, nullptr, vmsg.data(), vlens, v2_recovered ? 2 : 1, vsig.data(), &bm, &fb, vcls);
-  if (rc) return rc;
+  if (vc1 >= 0 && (!v2_recovered || vc2 >= 0)) {  // both verdicts already computed speculatively
+    bm = (uint8_t)((vc1 == BLSV_REJ_OK) | ((v2_recovered && vc2 == BLSV_REJ_OK) << 1));
+  } else {
+    rc = blsv_verify_messages(c, nullptr, vmsg.data(), vlens, v2_recovered ? 2 : 1, vsig.data(), &bm, &fb, vcls);
+    if (rc) return rc;
+  }
   if (!(bm & 1)) {
     *status = BLSV_AGG_V1_INVALID;  // chain.go:141-144 "invalid_sig": no beacon
     return BLSV_OK;

@@ -189,7 +189,7 @@ struct blsv_ctx {
   // speculative recovery beside a round's partial verification (blsverify.cpp spec_recover_*): two
   // slots (V1, V2), each with its decoded shares, Lagrange coefficients, products and output
   struct SpecSlot {
-    DBuf sig, S, s_inf, cls, sel, idx, lam, scratch, out;
+    DBuf sig, S, s_inf, cls, sel, idx, lam, scratch, out, vmsg, voff, vlen, vcls;
     PinBuf host;  // staged sigma bytes + indices in, the 96-byte result out (async copies only)
   } spec[2];
   uint64_t spec_hits = 0, spec_misses = 0;  // speculative recoveries kept / recomputed

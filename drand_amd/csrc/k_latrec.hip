@@ -1,5 +1,5 @@
 // tbls Recover's interpolation sum_i [lambda_i] S_i in the latency engine's lane form (wrecover.h):
-// one wave per selected share for the scalar multiplication, then one 8-wave workgroup for the
+// four waves per selected share for the scalar multiplication, then one 8-wave workgroup for the
 // sum, the affine conversion and the compression. Replaces a one-lane-per-share ladder whose
 // 255 serial doublings dominated a threshold round.
 #define WV_WAVES 8
@@ -10,25 +10,39 @@ namespace blsk {
 
 constexpr int SUM_WAVES = WV_WAVES;
 
-// scratch[i] <- [lambda_i] S[sel[i]] (Jacobian, POINT_WORDS words in lane order)
-__global__ void __launch_bounds__(64) k_lat_recover_mul(const uint32_t* S, size_t n_s, const uint8_t* s_inf,
-                                                        const uint32_t* sel, const uint32_t* lambdas, uint32_t t,
-                                                        uint32_t* scratch) {
-  __shared__ uint32_t tab[15 * wv::POINT_WORDS];
+// scratch[i] <- [lambda_i] S[sel[i]] (Jacobian, POINT_WORDS words in lane order): four waves per share,
+// wave j computing [d_j] P_j of lambda's x-adic digits (wrecover.h g2_mul_digit), wave 0 summing the
+// four products. Each wave's 63 doublings and ~32 mixed additions replace one wave's 63 doublings and
+// ~60 full additions of the joint table (g2_mul_lambda), and the four run on the CU's four SIMDs.
+constexpr int MUL_WAVES = 4;
+__global__ void __launch_bounds__(64 * MUL_WAVES) k_lat_recover_mul(const uint32_t* S, size_t n_s,
+                                                                    const uint8_t* s_inf, const uint32_t* sel,
+                                                                    const uint32_t* lambdas, uint32_t t,
+                                                                    uint32_t* scratch) {
+  __shared__ uint32_t part[(MUL_WAVES - 1) * wv::POINT_WORDS];
   const uint32_t i = blockIdx.x;
   if (i >= t) return;
   wv::wv_init();
+  const int j = threadIdx.x >> 6;
   const size_t k = sel[i];
-  wv::G2J r;
-  if (s_inf[k]) {
-    r = wv::g2_infinity();
-  } else {
+  const bool inf = s_inf[k] != 0;
+  wv::G2J r = wv::g2_infinity();
+  if (!inf) {
     uint32_t lam[8];
     for (int w = 0; w < 8; w++) lam[w] = lambdas[i * 8 + w];
+    uint64_t d[4];
+    wv::decompose_xabs(lam, d);
     const wv::F x = wv::fp2_from392(S, n_s, k, 0), y = wv::fp2_from392(S, n_s, k, 2);
-    r = wv::g2_mul_lambda(x, y, lam, tab);
+    wv::F px, py;
+    wv::lambda_base(x, y, j, px, py);
+    r = wv::g2_mul_digit(px, py, d[j]);
   }
-  wv::st_point(scratch + (size_t)i * wv::POINT_WORDS, r, true);
+  if (j > 0) wv::st_point(part + (j - 1) * wv::POINT_WORDS, r, false);
+  __syncthreads();
+  if (j == 0) {
+    for (int q = 0; q < MUL_WAVES - 1; q++) r = wv::g2_add(r, wv::ld_point(part + q * wv::POINT_WORDS, false));
+    wv::st_point(scratch + (size_t)i * wv::POINT_WORDS, r, true);
+  }
 }
 
 // out96 <- compress(sum of scratch[0 .. t)): strided partial sums per wave, then a tree in LDS
@@ -55,7 +69,8 @@ __global__ void __launch_bounds__(64 * SUM_WAVES) k_lat_recover_sum(const uint32
 void launch_lat_recover(const uint32_t* S, size_t n_s, const uint8_t* s_inf, const uint32_t* sel,
                         const uint32_t* lambdas, uint32_t t, uint32_t* scratch, uint8_t* out96, hipStream_t st) {
   if (!t) return;
-  hipLaunchKernelGGL(k_lat_recover_mul, dim3(t), dim3(64), 0, st, S, n_s, s_inf, sel, lambdas, t, scratch);
+  hipLaunchKernelGGL(k_lat_recover_mul, dim3(t), dim3(64 * MUL_WAVES), 0, st, S, n_s, s_inf, sel, lambdas, t,
+                     scratch);
   hipLaunchKernelGGL(k_lat_recover_sum, dim3(1), dim3(64 * SUM_WAVES), 0, st, scratch, t, out96);
 }
 

@@ -50,6 +50,22 @@ WVI G2J g2_add(const G2J& p, const G2J& q) {
   return {X3, Y3, Z3};
 }
 
+// p + q for an affine q (z = 1) with no exceptional-case tests (madd-2007-bl): the caller guarantees
+// p != +-q and neither is infinity -- as in a left-to-right ladder [k] q, 2 <= k < r, whose
+// intermediate multiples never equal +-q (wrecover.h). Ten products against add-2007-bl's fifteen
+// and its four zero tests.
+WVI G2J g2_madd_noexc(const G2J& p, const F& qx, const F& qy) {
+  const F Z1Z1 = sqr2(p.z);
+  const F H = dot(qx, Z1Z1, p.x, cst(WC_NEG1));                          // U2 - X1
+  const F r = dot(dot(qy, p.z), dbl(Z1Z1), p.y, cst(WC_NEG2));           // 2 (S2 - Y1)
+  const F I = dot(H, mul_small<4>(H));                                    // (2H)^2
+  const F J = dot(H, I), V = dot(p.x, I);
+  const F X3 = dot(r, r, J, cst(WC_NEG1), V, cst(WC_NEG2));
+  const F Y3 = dot(r, V, neg<0>(X3), r, p.y, neg<0>(dbl(J)));
+  const F Z3 = dot(p.z, dbl(H));                                          // 2 Z1 H
+  return {X3, Y3, Z3};
+}
+
 // projective equality (either may be infinity)
 WVI bool g2_eq(const G2J& p, const G2J& q) {
   const bool pi = g2_is_inf(p), qi = g2_is_inf(q);

@@ -107,6 +107,37 @@ WVI G2J g2_mul_lambda(const F& x, const F& y, const uint32_t (&lam)[8], uint32_t
   return acc;
 }
 
+// The same product split over four waves (k_lat_recover_mul): wave j computes [d_j] P_j alone, P_j
+// affine, by a left-to-right ladder of 63 doublings and one mixed addition per set bit below the top
+// one. Its intermediate multiples [k] P_j, 2 <= k < 2^64 < r, never equal +-P_j for P_j of order r,
+// so the addition needs no exceptional-case tests (g2_madd_noexc); a share outside G2 gives garbage
+// here, but its partial then fails verification and the speculative result is discarded.
+WVI G2J lambda_base(const F& x, const F& y, int j, F& px, F& py) {  // P_j, affine
+  px = x;
+  py = y;
+  if (j >= 2) {
+    px = mulp(x, cst(WC_PSI2_KX));
+    py = mulp(y, cst(WC_PSI2_KY));
+  }
+  if (j & 1) {
+    const G2J q = neg_psi_affine(px, py);
+    px = q.x;
+    py = q.y;
+  }
+  return {px, py, cst(WC_ONE2)};
+}
+WVI G2J g2_mul_digit(const F& qx, const F& qy, uint64_t k) {
+  if (!k) return g2_infinity();
+  const int top = 63 - __builtin_clzll(k);
+  G2J acc = {qx, qy, cst(WC_ONE2)};
+#pragma unroll 1
+  for (int b = top - 1; b >= 0; b--) {
+    acc = g2_dbl(acc);
+    if ((k >> b) & 1u) acc = g2_madd_noexc(acc, qx, qy);
+  }
+  return acc;
+}
+
 // ZCash compressed encoding of a point, as 24 big-endian words (lane j < 24 returns word j)
 WVI V g2_compress_words(const G2J& p) {
   const V l = lane_id();

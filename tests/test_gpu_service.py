@@ -76,6 +76,9 @@ def _mixed_partials(golden):
     return [bad[i] for i in range(len(parts))]
 
 
+BURSTS = 8
+
+
 def test_service_64_concurrent_partials(svc, golden, C):
     th = golden["threshold"]
     commits = [bytes.fromhex(c) for c in th["commits"]]
@@ -97,14 +100,15 @@ def test_service_64_concurrent_partials(svc, golden, C):
     lone_s = sorted(lone)[len(lone) // 2]
     l0, i0, _ = svc.stats()
     best = None
-    # the best of five bursts (host thread start-up jitter); a short GIL switch interval so that the
+    # the best of eight bursts (host thread start-up jitter: ~1-2 ms of it against a ~2 ms lone call);
+    # a short GIL switch interval so that the
     # 64 Python threads reach their ctypes calls together (the default 5 ms interval can hold the
     # late ones back past the service's coalescing window -- a Python artefact: the plain-C burst in
     # tools/cabi_smoke.c measures the same contract with pthreads)
     old_iv = sys.getswitchinterval()
     sys.setswitchinterval(1e-5)
     try:
-        for _ in range(5):
+        for _ in range(BURSTS):
             res, dt = _burst(calls)
             assert [c for _, c in res] == want
             assert [ok for ok, _ in res] == [c == 0 for c in want]
@@ -114,8 +118,8 @@ def test_service_64_concurrent_partials(svc, golden, C):
     l1, i1, mb = svc.stats()
     print(f"lone {lone_s * 1e3:.2f} ms, 64 concurrent {best * 1e3:.2f} ms, {l1 - l0} launches for {i1 - i0} items, "
           f"largest batch {mb}")
-    assert i1 - i0 == 5 * 64
-    assert l1 - l0 <= 10  # coalesced: at most two launches per burst
+    assert i1 - i0 == BURSTS * 64
+    assert l1 - l0 <= 2 * BURSTS  # coalesced: at most two launches per burst
     assert best <= 2.0 * lone_s, (best, lone_s)
 
 

@@ -134,3 +134,17 @@ def test_verify_mixed_golden_classes(wvtest, golden, cmd):
         prev = seed if i == 0 else sigs[i - 1]
         lines.append("%s %s %s" % (m["pk"], O.message(i + 1, prev).hex(), s.hex()))
     assert [int(x) for x in run(wvtest, cmd, lines)] == m["expect_class"]
+
+
+def test_recover_four_wave_lambda_product(wvtest, golden):
+    """wrecover.h's four-wave form of [lambda] S (k_lat_recover_mul: wave j computes [d_j] P_j with
+    the exception-free mixed addition) against the joint-table g2_mul_lambda, for the golden partials'
+    signatures and scalars below r: small ones, one-digit ones, and random full-width ones."""
+    import random
+    rng = random.Random(7)
+    r = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    x = 0xD201000000010000
+    sigs = [p[4:] for p in golden["threshold"]["partials"][:6]]
+    ks = [1, 2, 3, x - 1, x, x + 1, x * x + 5, r - 1] + [rng.randrange(1, r) for _ in range(10)]
+    lines = ["%s %x" % (sigs[i % len(sigs)], k) for i, k in enumerate(ks)]
+    assert run(wvtest, "smul4", lines) == ["ok"] * len(lines)

@@ -290,6 +290,42 @@ static int cmd_smul() {
   return 0;
 }
 
+// smul4: "sig96 k" -> "ok" when the four-wave form (wrecover.h lambda_base, g2_mul_digit per digit,
+// the four partial products summed) equals g2_mul_lambda's [k] S, else "bad"
+static int cmd_smul4() {
+  static uint32_t tab[15 * POINT_WORDS];
+  char a[300], b[300];
+  while (scanf("%299s %299s", a, b) == 2) {
+    wv_init();
+    const auto sig = unhex(a);
+    F x, y;
+    bool inf;
+    if (g2_decompress(sig.data(), x, y, inf) || inf) {
+      printf("-\n");
+      continue;
+    }
+    uint32_t lam[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const std::string h(b);
+    for (int i = 0; i < (int)h.size(); i++) {
+      const char c = h[h.size() - 1 - i];
+      const uint32_t v = c <= '9' ? c - '0' : (c | 32) - 'a' + 10;
+      lam[i / 8] |= v << (4 * (i % 8));
+    }
+    const G2J ref = g2_mul_lambda(x, y, lam, tab);
+    uint64_t d[4];
+    decompose_xabs(lam, d);
+    G2J sum = g2_infinity();
+    for (int j = 0; j < 4; j++) {
+      F px, py;
+      lambda_base(x, y, j, px, py);
+      sum = g2_add(sum, g2_mul_digit(px, py, d[j]));
+    }
+    printf(g2_eq(sum, ref) ? "ok\n" : "bad\n");
+    fflush(stdout);
+  }
+  return 0;
+}
+
 // teamadd: "sig96 case" -> ok / bad: wvteam.h team_g2_add (three host threads as the hash team's
 // waves 0, 4, 5) against wcurve.h g2_add for case sum (P' + 2P), dbl (P' + P), neg (P' + (-P)),
 // ainf (O + 2P), binf (P' + O), with P' = P in scaled Jacobian coordinates (Z = x_P); and "chain"
@@ -347,6 +383,7 @@ int main(int argc, char** argv) {
   if (argc >= 2 && !strcmp(argv[1], "decompress")) return cmd_decompress();
   if (argc >= 2 && !strcmp(argv[1], "opcount")) return cmd_opcount();
   if (argc >= 2 && !strcmp(argv[1], "smul")) return cmd_smul();
+  if (argc >= 2 && !strcmp(argv[1], "smul4")) return cmd_smul4();
   fprintf(stderr, "usage: wvtest field|verify|hash|pair\n");
   return 2;
 }
