@@ -589,6 +589,12 @@ WVI void team_miller_dbl(Team& t, const MPair& m, int tb, int& cur) {
     // waves 0..5 the six f^2 l coefficients (three-term products), wave 6 X3 and Z3, wave 7 Y3
     dbl_job2(t.id, tb, fout);
     if (t.id == 6) dbl_job2(8, tb, fout);
+  } else if (t.n == 4) {
+    // two three-term products per wave, the one-product X3 and Z3 with the fifth, the two-term Y3
+    // with the sixth (at most two products' worth per wave instead of three for the strided split)
+    constexpr uint8_t J[4][3] = {{0, 1, 9}, {2, 3, 9}, {4, 6, 8}, {5, 7, 9}};
+    for (int q = 0; q < 3; q++)
+      if (J[t.id][q] < 9) dbl_job2(J[t.id][q], tb, fout);
   } else {
     for (int j = t.id; j < 9; j += t.n) dbl_job2(j, tb, fout);
   }
