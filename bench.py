@@ -111,13 +111,17 @@ def cpu_baseline(pk48, segments, workers):
     return n / dt, sum(oks), n
 
 
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def launch_ranks(n):
     """Start n ranks of this script under torch.distributed.run as a CHILD process (never an exec:
     this process has not touched the GPU, and the ranks must each initialise their own) and return
     its exit status."""
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    port = free_port()
     # torch.distributed.run's parser would take "--n" as an abbreviation of its own options
     argv = ["--beacons-per-gpu" if a == "--n" else "--beacons-per-gpu=" + a[4:] if a.startswith("--n=") else a
             for a in sys.argv[1:]]
@@ -178,6 +182,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="exchange backend for N>1: nccl (= RCCL over xGMI, one GPU per rank) or gloo (host "
                          "copies; ranks may share a GPU)")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="form the --dist-backend process group and run the exchange (shard.combine) even at one "
+                         "rank: executes the RCCL branch on a one-GPU box (world size 1)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, form the process group, run one exchange on host tensors and print "
                          "one JSON line per rank, without touching a GPU (CPU test of the N-rank launch)")
@@ -204,8 +211,13 @@ def main():
         raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs, this node shows {ndev} "
                          "(--dist-backend gloo lets ranks share a GPU)")
     dev_idx = local % max(ndev, 1)
-    if world > 1:
+    use_pg = world > 1 or args.force_pg
+    if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:  # --force-pg without a launcher: a one-rank group by env init
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
         torch.cuda.set_device(dev_idx)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
@@ -283,7 +295,7 @@ def main():
     def step():
         eng.verify_chained_dev(first_round, seg, seeds.data_ptr(), seed0_len, sigs.data_ptr(), n,
                                bitmap.data_ptr(), first_bad.data_ptr(), None, sp, seg_phase=phase)
-        if world > 1:
+        if use_pg:
             # ONE SUM all-reduce: global-position bitmap + per-rank first bad ROUND slots (RCCL over xGMI)
             return shard.combine(first_bad, bitmap, n, to_host=False, counts=counts)
         return first_bad, bitmap
@@ -291,7 +303,7 @@ def main():
     def verdicts():
         fb, bm = step()
         torch.cuda.synchronize(dev)
-        total = sum(counts) if world > 1 else n
+        total = sum(counts) if use_pg else n
         ok = np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little")[:total].astype(bool)
         fbv = int(fb.item()) & (2 ** 64 - 1)
         return (None if fbv in (2 ** 64 - 1, shard.NONE_I64) else fbv), ok
@@ -316,37 +328,37 @@ def main():
     sigs[bad_i, 50] ^= 1  # bit flip in x.c0
     fbv, ok = verdicts()
     sigs[bad_i].copy_(saved)
-    gate = list(zip(counts, phases)) if world > 1 else [(n, phase)]
+    gate = list(zip(counts, phases)) if use_pg else [(n, phase)]
     want = np.ones(len(ok), bool)
     for r, (c, ph) in enumerate(gate):
         off, b = sum(x[0] for x in gate[:r]), bad_index(c, ph)
         want[off + b] = False
         if b + 1 < c:
             want[off + b + 1] = False
-    want_fb = (first_round - (sum(counts[:rank]) if world > 1 else 0)) + bad_index(*gate[0])
+    want_fb = (first_round - (sum(counts[:rank]) if use_pg else 0)) + bad_index(*gate[0])
     assert (ok == want).all() and fbv == want_fb, f"negative control failed: first_bad={fbv} want {want_fb} " \
         f"rejected={np.flatnonzero(~ok)[:8].tolist()}"
 
     eng.profile(True)
     eng.profile_read()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_pg:
         dist.barrier()
     dt = time.perf_counter() - t0
     prof = eng.profile_read()
     eng.profile(False)
-    if world > 1:  # the job's time is the slowest rank's
+    if use_pg:  # the job's time is the slowest rank's
         t = torch.tensor([dt], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    total = (sum(counts) if world > 1 else n) * args.steps
+    total = (sum(counts) if use_pg else n) * args.steps
     value = total / dt
     ms_per_step = dt * 1e3 / args.steps
 
@@ -406,7 +418,7 @@ def main():
         "gate": "all rounds accept; negative control (one bit-flipped signature per rank) rejects exactly it and "
                 "the next round, first_bad = lowest corrupted round",
     }
-    if world > 1:  # what the process group actually initialised (the exchange runs over it)
+    if use_pg:  # what the process group actually initialised (the exchange runs over it)
         devs = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
         if args.dist_backend == "gloo":
             dist.all_gather(devs, torch.tensor([dev_idx]))
@@ -443,7 +455,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -54,12 +54,15 @@ sz = ctypes.c_size_t
 # name -> (restype, argtypes); exactly the symbols of include/blsverify.h + blsverify_testing.h
 SIGNATURES = {
     "blsv_version": (ctypes.c_char_p, []),
+    "blsv_device_count": (ctypes.c_int, []),
     "blsv_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
     "blsv_destroy": (None, [vp]),
     "blsv_last_error": (ctypes.c_char_p, [vp]),
     "blsv_synchronize": (ctypes.c_int, [vp]),
     "blsv_set_group": (ctypes.c_int, [vp, u8p, sz, sz]),
     "blsv_verify_chained": (ctypes.c_int, [vp, ctypes.c_uint64, u8p, sz, u8p, sz, u8p, u64p, u8p]),
+    "blsv_verify_chained_multi": (ctypes.c_int, [ctypes.POINTER(vp), sz, ctypes.POINTER(sz), ctypes.c_uint64, u8p, sz,
+                                                  u8p, sz, u8p, u64p, u8p]),
     "blsv_verify_prevs": (ctypes.c_int, [vp, ctypes.c_uint64, u8p, sz, u8p, sz, u8p, u64p, u8p]),
     "blsv_verify_unchained": (ctypes.c_int, [vp, u64p, ctypes.c_uint64, u8p, sz, u8p, u64p, u8p]),
     "blsv_verify_messages": (ctypes.c_int, [vp, u8p, u8p, u32p, sz, u8p, u8p, u64p, u8p]),
@@ -91,6 +94,7 @@ SIGNATURES = {
     "blsv_service_verify_partial": (ctypes.c_int, [vp, u8p, sz, sz, u8p, sz, u8p, sz, u8p, u8p]),
     "blsv_service_verify_recovered": (ctypes.c_int, [vp, u8p, u8p, sz, u8p, u8p, u8p]),
     "blsv_service_stats": (ctypes.c_int, [vp, u64p, u64p, u64p]),
+    "blsv_test_service_limits": (ctypes.c_int, [vp, sz, sz, sz, u64p]),
 }
 
 _lib = None

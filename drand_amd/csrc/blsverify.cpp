@@ -11,6 +11,7 @@
 #include <cstring>
 #include <string>
 #include <cstdlib>
+#include <thread>
 #include <vector>
 
 #include "../../include/blsverify.h"
@@ -408,9 +409,11 @@ int svc_verify_mixed(blsv_ctx* c, size_t n, const uint8_t* msgs, const uint64_t*
     HIPCHK(c, c->bitmap.ensure(words * 8 + 8));
     HIPCHK(c, c->first_bad.ensure(8));
     HIPCHK(c, hipMemsetAsync(c->first_bad.p, 0xff, 8, c->stream));
-    const PkSel pk{d_tab, d_tab_inf, d_idx};
     for (size_t base = 0; base < n; base += c->cap) {
       const size_t cnt = std::min(c->cap, n - base);
+      // the Miller stage indexes pk_idx by the chunk-local item: hand it this pass's slice of the
+      // per-item key entries (a batch spans several passes once an OOM halving shrank the chunk)
+      const PkSel pk{d_tab, d_tab_inf, d_idx + base};
       rc = run_head(c, d_sig, 96, 0, base, cnt, c->stream, [&]() {
         blsk::launch_hash_messages(d_msg, d_off + base, d_len + base, cnt, c->H.as<uint32_t>(), c->h_inf.as<uint8_t>(),
                                    c->HQ.as<uint32_t>(), c->stream);
@@ -431,6 +434,11 @@ int svc_verify_mixed(blsv_ctx* c, size_t n, const uint8_t* msgs, const uint64_t*
 extern "C" {
 
 const char* blsv_version(void) { return "drand_amd blsverify 0.1 (gfx950)"; }
+
+int blsv_device_count(void) {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
 
 int blsv_create(int device, blsv_ctx** out) {
   if (!out) return BLSV_EINVAL;
@@ -531,6 +539,71 @@ int blsv_verify_chained(blsv_ctx* c, uint64_t first_round, const uint8_t* prev0,
       [&](uint8_t* cls) { blsk::launch_lat_chained(src, 0, n, pk.tab, pk.inf, cls, c->stream); }, true);
   if (rc) return rc;
   if (first_bad) *first_bad = fb == UINT64_MAX ? UINT64_MAX : first_round + fb;
+  return BLSV_OK;
+}
+
+// OR the first cnt bits of src (LSB first) into dst starting at bit pos
+static void or_bits_at(uint8_t* dst, const uint8_t* src, size_t cnt, size_t pos) {
+  const size_t nb = (cnt + 7) / 8, q = pos / 8, s = pos % 8;
+  for (size_t j = 0; j < nb; j++) {
+    uint8_t b = src[j];
+    if (j == nb - 1 && (cnt % 8)) b &= (uint8_t)((1u << (cnt % 8)) - 1);
+    dst[q + j] |= (uint8_t)(b << s);
+    if (s && (b >> (8 - s))) dst[q + j + 1] |= (uint8_t)(b >> (8 - s));
+  }
+}
+
+int blsv_verify_chained_multi(blsv_ctx* const* ctxs, size_t n_ctx, const size_t* shard_counts, uint64_t first_round,
+                              const uint8_t* prev0, size_t prev0_len, const uint8_t* sigs96, size_t n,
+                              uint8_t* ok_bitmap, uint64_t* first_bad, uint8_t* reject_class) {
+  if (!ctxs || n_ctx == 0) return BLSV_EINVAL;
+  for (size_t k = 0; k < n_ctx; k++) {
+    if (!ctxs[k]) return BLSV_EINVAL;
+    for (size_t j = 0; j < k; j++)
+      if (ctxs[j] == ctxs[k]) return fail(ctxs[k], BLSV_EINVAL, "verify_chained_multi: context %zu repeated", k);
+  }
+  blsv_ctx* c0 = ctxs[0];
+  for (size_t k = 0; k < n_ctx; k++) {
+    if (!ctxs[k]->has_group) return fail(ctxs[k], BLSV_ENOGROUP, "verify_chained_multi: context %zu has no group", k);
+    if (ctxs[k]->group_bytes != c0->group_bytes)
+      return fail(ctxs[k], BLSV_EINVAL, "verify_chained_multi: context %zu holds another group", k);
+  }
+  if (n && (!sigs96 || !prev0 || (prev0_len != 32 && prev0_len != 96)))
+    return fail(c0, BLSV_EINVAL, "verify_chained_multi: prev0 must be 32 or 96 bytes");
+  std::vector<size_t> cnt(n_ctx), start(n_ctx);
+  size_t sum = 0;
+  for (size_t k = 0; k < n_ctx; k++) {
+    cnt[k] = shard_counts ? shard_counts[k] : n / n_ctx + (k < n % n_ctx ? 1 : 0);
+    start[k] = sum;
+    sum += cnt[k];
+  }
+  if (sum != n) return fail(c0, BLSV_EINVAL, "verify_chained_multi: shard counts sum to %zu, not %zu", sum, n);
+  std::vector<std::vector<uint8_t>> bms(n_ctx);
+  std::vector<uint64_t> fbs(n_ctx, UINT64_MAX);
+  std::vector<int> rcs(n_ctx, BLSV_OK);
+  auto shard = [&](size_t k) {
+    if (!cnt[k]) return;
+    bms[k].assign((cnt[k] + 7) / 8, 0);
+    const bool head = start[k] == 0;
+    const uint8_t* halo = head ? prev0 : sigs96 + (start[k] - 1) * 96;  // the true PreviousSig of its first round
+    rcs[k] = blsv_verify_chained(ctxs[k], first_round + start[k], halo, head ? prev0_len : 96, sigs96 + start[k] * 96,
+                                 cnt[k], bms[k].data(), &fbs[k], reject_class ? reject_class + start[k] : nullptr);
+  };
+  std::vector<std::thread> th;
+  for (size_t k = 1; k < n_ctx; k++)
+    if (cnt[k]) th.emplace_back(shard, k);
+  shard(0);
+  for (auto& t : th) t.join();
+  for (size_t k = 0; k < n_ctx; k++)
+    if (rcs[k]) return rcs[k];
+  uint64_t fb = UINT64_MAX;
+  for (size_t k = 0; k < n_ctx; k++) fb = std::min(fb, fbs[k]);
+  if (first_bad) *first_bad = fb;
+  if (ok_bitmap && n) {
+    memset(ok_bitmap, 0, (n + 7) / 8);
+    for (size_t k = 0; k < n_ctx; k++)
+      if (cnt[k]) or_bits_at(ok_bitmap, bms[k].data(), cnt[k], start[k]);
+  }
   return BLSV_OK;
 }
 
@@ -953,6 +1026,20 @@ static int spec_recover_finish(blsv_ctx* c, int slot, const SpecRecover& sr, con
   return recover_from(c, cls, index, lo, hi, t, n, out_sig96);
 }
 
+// Drains both side streams when a call that launched speculative work returns, on every path: an
+// early error return must not leave async copies into the slots' pinned staging in flight (the next
+// call's spec_recover_launch writes that staging without a synchronisation when it is large enough).
+// On the normal path spec_recover_finish has drained `side` already and this costs two idle syncs.
+struct SideDrain {
+  blsv_ctx* c;
+  bool armed = false;
+  ~SideDrain() {
+    if (!armed) return;
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamSynchronize(c->side2);
+  }
+};
+
 // partial_len == 98 and the round small enough for the latency path (partials_stage's choice)
 static bool spec_applies(const blsv_ctx* c, size_t k, size_t partial_len) {
   return partial_len == 98 && c->has_group && k > 0 && k <= std::min(c->lat_max, c->chunk);
@@ -973,16 +1060,15 @@ int blsv_aggregate(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_
   std::vector<uint8_t> cls;
   std::vector<uint32_t> index;
   SpecRecover sr;
+  SideDrain drain{c};
   if (spec_applies(c, k, partial_len)) {
     share_indices(partials, partial_len, k, index);
+    drain.armed = true;
     int rc0 = spec_recover_launch(c, 0, partials, partial_len, index, 0, k, t, n, sr, msg, msg_len);
     if (rc0) return rc0;
   }
   int rc = partials_stage(c, msg, msg_len, partials, partial_len, k, cls, index);
-  if (rc) {
-    if (sr.launched) (void)hipStreamSynchronize(c->side);
-    return rc;
-  }
+  if (rc) return rc;
   for (size_t i = 0; i < k; i++) {
     ok[i] = cls[i] == BLSV_REJ_OK;
     if (reject_class) reject_class[i] = cls[i];
@@ -1036,31 +1122,24 @@ int blsv_aggregate_round(blsv_ctx* c, const uint8_t* msg1, size_t msg1_len, cons
   std::vector<uint32_t> index;
   const bool try_v2 = k2 >= t;
   SpecRecover sr1, sr2;  // both recoveries speculated on the side stream (see spec_recover_launch)
+  SideDrain drain{c};
   if (spec_applies(c, k, partial_len)) {
     share_indices(parts.data(), partial_len, k, index);
+    drain.armed = true;
     int rc0 = spec_recover_launch(c, 0, parts.data(), partial_len, index, 0, k1, t, n, sr1, msg1 ? msg1 : parts.data(),
                                   msg1_len);
     if (!rc0 && try_v2)
       rc0 = spec_recover_launch(c, 1, parts.data(), partial_len, index, k1, k, t, n, sr2, msg2, msg2_len);
-    if (rc0) {
-      (void)hipStreamSynchronize(c->side);
-      return rc0;
-    }
+    if (rc0) return rc0;
   }
   int rc = partials_stage(c, msgs.data(), 0, parts.data(), partial_len, k, cls, index, lens.data());
-  if (rc) {
-    if (sr1.launched || sr2.launched) (void)hipStreamSynchronize(c->side);
-    return rc;
-  }
+  if (rc) return rc;
   for (size_t i = 0; i < k1; i++) ok1[i] = cls[i] == BLSV_REJ_OK;
   for (size_t i = 0; i < k2; i++) ok2[i] = cls[k1 + i] == BLSV_REJ_OK;
   // Recover V1 (chain.go:136) and, with LenV2 >= thr, V2 (chain.go:153-155) from the staged shares
   int vc1 = -1, vc2 = -1;
   rc = spec_recover_finish(c, 0, sr1, cls, index, 0, k1, t, n, sig1_96, &vc1);
-  if (rc == BLSV_ENOTENOUGH) {
-    if (sr2.launched) (void)hipStreamSynchronize(c->side);
-    return BLSV_OK;  // "invalid_recovery": no beacon this time
-  }
+  if (rc == BLSV_ENOTENOUGH) return BLSV_OK;  // "invalid_recovery": no beacon this time (drain syncs sr2)
   if (rc) return rc;
   bool v2_recovered = false;
   if (try_v2) {

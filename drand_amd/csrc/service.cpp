@@ -70,6 +70,8 @@ struct blsv_service {
   std::vector<std::unique_ptr<GroupEnt>> groups;
   std::vector<KeyEnt> keys;
   DBuf in48, cls48, idx;       // decode / Horner staging
+  size_t arena_cap = kArenaEntries;  // entries usable (lowered only by blsv_test_service_limits)
+  uint64_t launches = 0;       // svc_verify_mixed calls (sub-batches included)
   std::unique_ptr<Coalescer<SvcItem>> co;
 
   void reset_arena() {
@@ -115,17 +117,18 @@ struct blsv_service {
     return nullptr;
   }
 
-  // installs a group: commitments decoded, PK_i table built; nullptr + *rc on a bad commitment
-  GroupEnt* add_group(const SvcItem& it, int* rc) {
+  // installs a group: commitments decoded, PK_i table built; nullptr + *rc on a bad commitment.
+  // `reserve` entries above `used` are already promised to this sub-batch's out-of-table indices.
+  GroupEnt* add_group(const SvcItem& it, size_t reserve, int* rc) {
     const size_t m = std::min(it.n, kPkTable);
-    if (used + m > kArenaEntries) return nullptr;  // caller resets the arena
+    *rc = BLSV_OK;
+    if (used + m + reserve > arena_cap) return nullptr;  // the sub-batch ends here
     auto g = std::make_unique<GroupEnt>();
     g->bytes.assign(it.commits, it.commits + it.t * 48);
     g->t = it.t;
     g->n = it.n;
     g->m = m;
     g->off = used;
-    *rc = BLSV_OK;
     if (g->commits.ensure(it.t * blsk::G1_WORDS * 4) != hipSuccess || g->commit_inf.ensure(it.t) != hipSuccess) {
       *rc = fail(c, BLSV_EHIP, "service: commitment staging");
       return nullptr;
@@ -145,9 +148,9 @@ struct blsv_service {
     return groups.back().get();
   }
 
-  KeyEnt* add_key(const uint8_t* pk48, int* rc) {
+  KeyEnt* add_key(const uint8_t* pk48, size_t reserve, int* rc) {
     *rc = BLSV_OK;
-    if (used + 1 > kArenaEntries) return nullptr;
+    if (used + 1 + reserve > arena_cap) return nullptr;  // the sub-batch ends here
     std::vector<uint8_t> cls;
     if ((*rc = decode_into(pk48, 1, tab.as<uint32_t>() + used * blsk::G1_WORDS, tab_inf.as<uint8_t>() + used, cls)))
       return nullptr;
@@ -162,78 +165,73 @@ struct blsv_service {
     return &keys.back();
   }
 
-  // resolves every item's arena entry (items with rc != 0 drop out); false when the arena overflowed
-  bool resolve(std::vector<SvcItem*>& b, std::vector<std::pair<GroupEnt*, SvcItem*>>& beyond) {
-    for (SvcItem* it : b) {
+  // Resolves the arena entries of b[pos, end) for the largest end whose keys fit the arena and returns
+  // end (items whose own key fails get rc != 0 and stay in the range). Out-of-table share indices are
+  // evaluated per sub-batch into the arena's tail, above every cached group and key.
+  size_t resolve(std::vector<SvcItem*>& b, size_t pos) {
+    std::vector<std::pair<GroupEnt*, SvcItem*>> beyond;
+    size_t i = pos;
+    for (; i < b.size(); i++) {
+      SvcItem* it = b[i];
+      it->entry = 0;
       if (it->rc) continue;
       int rc = BLSV_OK;
       if (it->partial) {
         GroupEnt* g = find_group(*it);
-        if (!g) g = add_group(*it, &rc);
+        if (!g) g = add_group(*it, beyond.size(), &rc);
         if (!g) {
           if (rc) {
             it->rc = rc;
             continue;
           }
-          return false;
+          break;
         }
-        if (it->index < g->m)
+        if (it->index < g->m) {
           it->entry = g->off + it->index;
-        else
-          beyond.push_back({g, it});  // an index >= n still has a well-defined Eval in kyber
+        } else {  // an index >= n still has a well-defined Eval in kyber
+          if (used + beyond.size() + 1 > arena_cap) break;
+          beyond.push_back({g, it});
+        }
       } else {
         KeyEnt* k = find_key(it->pk48);
-        if (!k) k = add_key(it->pk48, &rc);
+        if (!k) k = add_key(it->pk48, beyond.size(), &rc);
         if (!k) {
           if (rc) {
             it->rc = rc;
             continue;
           }
-          return false;
+          break;
         }
         it->entry = k->off;
       }
     }
-    if (used + beyond.size() > kArenaEntries) return false;
-    // per-batch Horner for out-of-table indices, one launch per group, into the arena's tail
+    // per-sub-batch Horner for the out-of-table indices, one launch per group
     std::stable_sort(beyond.begin(), beyond.end(),
                      [](const std::pair<GroupEnt*, SvcItem*>& a, const std::pair<GroupEnt*, SvcItem*>& b) {
                        return a.first < b.first;
                      });
     size_t tail = used;
-    for (size_t i = 0; i < beyond.size();) {
-      size_t j = i;
+    for (size_t q = 0; q < beyond.size();) {
+      size_t j = q;
       std::vector<uint32_t> ix;
-      for (; j < beyond.size() && beyond[j].first == beyond[i].first; j++) {
+      for (; j < beyond.size() && beyond[j].first == beyond[q].first; j++) {
         ix.push_back(beyond[j].second->index);
-        beyond[j].second->entry = tail + (j - i);
+        beyond[j].second->entry = tail + (j - q);
       }
-      const int rc = eval_into(*beyond[i].first, ix, tail);
+      const int rc = eval_into(*beyond[q].first, ix, tail);
       if (rc)
-        for (size_t q = i; q < j; q++) beyond[q].second->rc = rc;
-      tail += j - i;
-      i = j;
+        for (size_t r = q; r < j; r++) beyond[r].second->rc = rc;
+      tail += j - q;
+      q = j;
     }
-    return true;
+    return i;
   }
 
-  void run(std::vector<SvcItem*>& b) {
-    (void)hipSetDevice(c->device);
-    std::vector<std::pair<GroupEnt*, SvcItem*>> beyond;
-    for (SvcItem* it : b) it->entry = 0;
-    if (!resolve(b, beyond)) {  // arena full: keep only what this batch needs
-      reset_arena();
-      beyond.clear();
-      for (SvcItem* it : b) it->entry = 0;
-      if (!resolve(b, beyond)) {
-        for (SvcItem* it : b)
-          if (!it->rc) it->rc = fail(c, BLSV_EINVAL, "service: keys of one batch exceed the key arena");
-        return;
-      }
-    }
+  // one launch over the live items of b[lo, hi)
+  void launch(std::vector<SvcItem*>& b, size_t lo, size_t hi) {
     std::vector<SvcItem*> live;
-    for (SvcItem* it : b)
-      if (!it->rc) live.push_back(it);
+    for (size_t i = lo; i < hi; i++)
+      if (!b[i]->rc) live.push_back(b[i]);
     const size_t n = live.size();
     if (!n) return;
     std::vector<uint64_t> off(n + 1, 0);
@@ -252,6 +250,36 @@ struct blsv_service {
     for (size_t i = 0; i < n; i++) {
       live[i]->rc = rc;
       live[i]->cls = rc ? (uint8_t)BLSV_REJ_OK : cls[i];
+    }
+    launches++;
+  }
+
+  // A batch whose keys overflow the arena (many groups or keys, or out-of-table share indices: one tail
+  // entry each) runs as consecutive sub-batches, the arena rebuilt between them, so no caller fails
+  // because of what the others sent.
+  void run(std::vector<SvcItem*>& b) {
+    (void)hipSetDevice(c->device);
+    size_t pos = 0;
+    bool fresh = false;  // the arena holds nothing of an earlier sub-batch
+    while (pos < b.size()) {
+      const size_t end = resolve(b, pos);
+      if (end == pos) {  // b[pos]'s keys do not fit beside the cached ones
+        if (!fresh) {
+          reset_arena();
+          fresh = true;
+          continue;
+        }
+        b[pos]->rc = fail(c, BLSV_EINVAL, "service: one item's keys exceed the key arena");
+        pos++;
+        continue;
+      }
+      launch(b, pos, end);
+      pos = end;
+      fresh = false;
+      if (pos < b.size()) {
+        reset_arena();
+        fresh = true;
+      }
     }
   }
 };
@@ -274,8 +302,11 @@ int blsv_service_create(int device, uint32_t gap_us, uint32_t max_wait_us, blsv_
   }
   const uint32_t gap = gap_us ? gap_us : env_us("BLSV_SVC_GAP_US", 100);
   const uint32_t wait = max_wait_us ? max_wait_us : env_us("BLSV_SVC_MAX_WAIT_US", 2000);
-  s->co = std::make_unique<Coalescer<SvcItem>>([s](std::vector<SvcItem*>& b) { s->run(b); }, gap, wait,
-                                               kServiceMaxBatch);
+  s->co = std::make_unique<Coalescer<SvcItem>>([s](std::vector<SvcItem*>& b) { s->run(b); }, gap, wait, kServiceMaxBatch,
+      // run() threw (std::bad_alloc of a large batch's host staging): the call fails, the process lives
+      [](SvcItem* it) {
+        if (!it->rc) it->rc = BLSV_EHIP;
+      });
   *out = s;
   return BLSV_OK;
 }
@@ -335,6 +366,30 @@ int blsv_service_verify_recovered(blsv_service* s, const uint8_t* pk48, const ui
   *ok = it.cls == BLSV_REJ_OK;
   if (reject_class) *reject_class = it.cls;
   return BLSV_OK;
+}
+
+int blsv_test_service_limits(blsv_service* s, size_t chunk, size_t lat_max, size_t arena_entries,
+                             uint64_t* sub_launches) {
+  if (!s) return BLSV_EINVAL;
+  if (sub_launches) *sub_launches = s->launches;
+  if (!chunk && !lat_max && !arena_entries) return BLSV_OK;
+  // every field is only read by the dispatcher thread inside run(): take it out of service first
+  return s->co->with_idle([&] {
+    blsv_ctx* c = s->c;
+    (void)hipSetDevice(c->device);
+    if (chunk) {
+      (void)hipStreamSynchronize(c->stream);
+      (void)hipStreamSynchronize(c->side);
+      release_workspace(c);
+      c->chunk = (std::max<size_t>(chunk, 64) + 63) & ~size_t(63);  // below kMinChunk on purpose
+    }
+    c->lat_max = std::min(lat_max == SIZE_MAX ? c->lat_max : lat_max, c->chunk);
+    if (arena_entries) {
+      s->arena_cap = std::min(arena_entries, kArenaEntries);
+      s->reset_arena();
+    }
+    return BLSV_OK;
+  });
 }
 
 int blsv_service_stats(blsv_service* s, uint64_t* launches, uint64_t* items, uint64_t* max_batch) {

@@ -386,6 +386,31 @@ class Engine:
         self._check(self.lib.blsv_test_generic_chains(self._h, 1 if on else 0))
 
 
+def verify_chained_multi(engines, first_round, prev0, sigs, counts=None):
+    """blsv_verify_chained_multi: the chained range split into contiguous shards over several
+    Engines (one per GPU; each holds the same group), verified concurrently (one host thread per
+    context inside the library) and merged: the BatchResult of one verify_chained over the whole
+    range. counts: shard lengths (None = even split)."""
+    if not engines:
+        raise ValueError("verify_chained_multi needs at least one engine")
+    lib = engines[0].lib
+    n = len(sigs)
+    if any(len(s) != 96 for s in sigs):
+        raise ValueError("chained signatures must be 96 bytes (reject wrong lengths host-side)")
+    sigb = b"".join(bytes(s) for s in sigs)
+    hs = (ctypes.c_void_p * len(engines))(*[e._h.value for e in engines])
+    cs = None if counts is None else (ctypes.c_size_t * len(engines))(*counts)
+    bm = _lib.out_buf((n + 7) // 8)
+    fb = ctypes.c_uint64()
+    cls = _lib.out_buf(n)
+    rc = lib.blsv_verify_chained_multi(hs, len(engines), cs, first_round, _lib.buf(prev0), len(prev0), _lib.buf(sigb),
+                                       n, bm, ctypes.byref(fb), cls)
+    if rc != 0:
+        msgs = "; ".join(lib.blsv_last_error(e._h).decode(errors="replace") for e in engines)
+        raise EngineError(rc, f"blsv_verify_chained_multi failed: {msgs}")
+    return BatchResult(_bits(bm, n), None if fb.value == 2 ** 64 - 1 else fb.value, list(cls)[:n])
+
+
 class Service:
     """Thread-safe front end (blsv_service_*): any number of threads call verify_partial /
     verify_recovered at once; items that arrive together are verified in one launch. ctypes releases
@@ -454,6 +479,15 @@ class Service:
         if rc != 0:
             raise EngineError(rc, "blsv_service_verify_recovered failed")
         return bool(ok.value), cls.value
+
+    def test_limits(self, chunk=0, lat_max=(1 << 64) - 1, arena_entries=0):
+        """blsv_test_service_limits: shrink the dispatcher's pass size / cutover / key arena (tests of
+        the multi-pass and arena-overflow paths); returns the device batches run so far."""
+        n = ctypes.c_uint64()
+        rc = self.lib.blsv_test_service_limits(self._h, int(chunk), int(lat_max), int(arena_entries), ctypes.byref(n))
+        if rc != 0:
+            raise EngineError(rc, "blsv_test_service_limits failed")
+        return n.value
 
     def stats(self):
         """(launches, items, largest batch) since creation."""

@@ -78,6 +78,10 @@ typedef struct blsv_ctx blsv_ctx;
 /* Library version string. */
 const char* blsv_version(void);
 
+/* Number of GPUs this process sees (0 when none or on a HIP error): one context per GPU for
+ * blsv_verify_chained_multi. */
+int blsv_device_count(void);
+
 /* Create a context on HIP device `device`. */
 int blsv_create(int device, blsv_ctx** out);
 void blsv_destroy(blsv_ctx* ctx);
@@ -103,6 +107,25 @@ int blsv_set_group(blsv_ctx* ctx, const uint8_t* commits48, size_t t, size_t n);
 int blsv_verify_chained(blsv_ctx* ctx, uint64_t first_round, const uint8_t* prev0, size_t prev0_len,
                         const uint8_t* sigs96, size_t n, uint8_t* ok_bitmap, uint64_t* first_bad,
                         uint8_t* reject_class);
+
+/*
+ * blsv_verify_chained over SEVERAL contexts at once -- the multi-GPU shape of a Go host: one context
+ * per GPU (ctxs[k] may sit on any device; each must hold the same group, set with blsv_set_group, and
+ * appear once), one host thread per context. The range is split into n_ctx contiguous shards
+ * (shard_counts[k] beacons each, summing to n; NULL = an even split, the first n % n_ctx shards one
+ * longer); shard k's PreviousSig halo is the signature just before it (prev0 for the first shard), so
+ * a corrupted signature at a shard edge still fails its successor in the next shard. The shards run
+ * concurrently and their verdicts are merged in host memory: ok_bitmap / reject_class at their
+ * positions in the whole range, first_bad = the lowest rejected ROUND over the shards (UINT64_MAX =
+ * none). Identical outputs to one blsv_verify_chained call over the whole range. Replaces the serial
+ * loops of client/verify.go:146-163 and chain/beacon/sync.go:100-119 on a multi-GPU node without a
+ * collective (the shards share the caller's address space). Contexts are used by one thread each for
+ * the duration of the call. Returns the first failing shard's code (its message in
+ * blsv_last_error(ctxs[k])); BLSV_EINVAL for a bad split, a repeated context or differing groups.
+ */
+int blsv_verify_chained_multi(blsv_ctx* const* ctxs, size_t n_ctx, const size_t* shard_counts, uint64_t first_round,
+                              const uint8_t* prev0, size_t prev0_len, const uint8_t* sigs96, size_t n,
+                              uint8_t* ok_bitmap, uint64_t* first_bad, uint8_t* reject_class);
 
 /*
  * chain.VerifyBeacon (chain/beacon.go:87-92) over n consecutive rounds first_round.. where each

@@ -49,6 +49,18 @@ int blsv_test_generic_chains(blsv_ctx* ctx, int on);
 int blsv_test_spec_stats(blsv_ctx* ctx, uint64_t* hits, uint64_t* misses);
 
 /*
+ * Reconfigures a service's dispatcher context for the tests of its multi-pass and overflow paths
+ * (waits until no batch is running): chunk != 0 sets the pipeline pass size to chunk items rounded up
+ * to 64 (below the public floor kMinChunk on purpose, so that a small burst spans several passes);
+ * lat_max sets the latency-path cutover (SIZE_MAX keeps it; 0 = batch pipeline only); arena_entries
+ * != 0 caps the key arena (and empties it), so that a burst overflows it and runs as sub-batches.
+ * *sub_launches (may be NULL) receives the number of device batches the service has run so far (a
+ * coalesced batch split for the arena counts once per sub-batch). All three 0: only the count.
+ */
+int blsv_test_service_limits(blsv_service* svc, size_t chunk, size_t lat_max, size_t arena_entries,
+                             uint64_t* sub_launches);
+
+/*
  * Stage timing for bench.py's roofline: when enabled, every stage launch (0 hash, 1 decompress,
  * 2 miller, 3 final_exp, 4 finish, 5 lat = a whole batch on the latency path) is bracketed by HIP
  * events on its launch stream. blsv_profile_read waits for the recorded events, writes per-stage

@@ -3,7 +3,7 @@
 //   coalesce  the blsv_service request coalescer (drand_amd/csrc/coalesce.h) with a stand-in run():
 //             64 threads x rounds of bursts, every request answered exactly once with its own
 //             result, bursts coalesced, stats consistent, destruction drains; and a lone request
-//             leaves after the gap.
+//             leaves after the gap; a run() that throws fails only its own batch's calls.
 //   boltload  the drand.db loader (drand_amd/csrc/boltload.cpp, include/boltload.h) over the files
 //             named on the command line (written by tests/support/boltwriter.py), plus truncated and
 //             bit-flipped copies of each: every call must fail cleanly or succeed, never fault.
@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <new>
 #include <chrono>
 #include <string>
 #include <thread>
@@ -90,6 +91,37 @@ int test_coalesce() {
     CHECK(us < 1900);
   }  // destructor joins
   CHECK(seen.load() == 64 * 20 + 1);
+  // run() throwing (a std::bad_alloc of a large batch): every caller of that batch returns, marked
+  // failed by the fail hook, and the dispatcher serves the next batch
+  {
+    std::atomic<int> calls{0};
+    Coalescer<Req> co(
+        [&](std::vector<Req*>& b) {
+          if (calls++ == 0) throw std::bad_alloc();
+          for (Req* r : b) r->out = r->in + 1;
+        },
+        100, 1000, 64, [](Req* r) { r->out = -2; });
+    std::vector<std::thread> th;
+    std::vector<Req> qs(16);
+    for (int t = 0; t < 16; t++) {
+      qs[t].in = t;
+      th.emplace_back([&, t] { co.submit(&qs[t]); });
+    }
+    for (auto& x : th) x.join();
+    int failed = 0, served = 0;
+    for (int t = 0; t < 16; t++) {
+      failed += qs[t].out == -2;
+      served += qs[t].out == t + 1;
+    }
+    CHECK(failed >= 1 && failed + served == 16);
+    Req q;
+    q.in = 41;
+    co.submit(&q);
+    CHECK(q.out == 42);
+    // with_idle runs between batches
+    int v = co.with_idle([&] { return 5; });
+    CHECK(v == 5);
+  }
   printf("{\"coalesce\": {\"batches\": %llu, \"items\": %llu, \"largest\": %zu}}\n",
          (unsigned long long)batches.load(), (unsigned long long)seen.load(), largest.load());
   return 0;
