@@ -102,7 +102,9 @@ def test_service_64_concurrent_partials(svc, golden, C):
     grp = C.Group(commits)
     want = [grp.verify_partial(msg, p) for p in parts]
     assert sum(1 for c in want if c) == 4
-    assert want[3] == 7 and want[41] == 7 and want[63] == 7  # pairing rejects: flip, wrong index, V2 msg
+    # the flip at byte 50 lands in x.c0 of the signature: x^3 + 4(u + 1) has no root (NOT_ON_CURVE);
+    # the wrong index and the V2-message share reach the pairing and fail it
+    assert want[3] == 5 and want[20] == 6 and want[41] == 7 and want[63] == 7
 
     # arguments marshalled in advance: each thread holds the GIL only for its ctypes call
     calls = [svc.prepare_partial(commits, th["n"], msg, p) for p in parts]
