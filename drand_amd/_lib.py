@@ -89,6 +89,7 @@ SIGNATURES = {
     "blsv_lat_trace_enable": (ctypes.c_int, [vp, ctypes.c_int]),
     "blsv_test_generic_chains": (ctypes.c_int, [vp, ctypes.c_int]),
     "blsv_test_spec_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "blsv_test_lagrange": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32)]),
     "blsv_service_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(vp)]),
     "blsv_service_destroy": (None, [vp]),
     "blsv_service_verify_partial": (ctypes.c_int, [vp, u8p, sz, sz, u8p, sz, u8p, sz, u8p, u8p]),

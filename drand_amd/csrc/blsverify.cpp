@@ -171,6 +171,155 @@ static void scalar_mod_r(const uint8_t* be32, uint32_t out[8]) {
   }
 }
 
+// ---------------------------------------------------------------- Lagrange coefficients on the host
+// kyber share.RecoverCommit's basis at 0 ([ext] drand/kyber@d59c3367dcde share/poly.go, restated) over
+// Fr for the shares x_i = index_i + 1: lambda_i = prod_{j != i} x_j / (x_j - x_i). Every factor is a
+// small integer (|x_j - x_i| < 2^16), so a coefficient is ~2t small products and the t inverses share
+// one Fermat inversion (Montgomery's trick): ~30 us for t = 33 against 0.56 ms for the serial
+// one-lane-per-coefficient device kernel this replaced, and the recovery no longer waits on it.
+namespace hfr {
+typedef unsigned __int128 u128;
+static const uint64_t RM[4] = {0xffffffff00000001ull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull,
+                               0x73eda753299d7d48ull};
+struct E {
+  uint64_t l[4];
+};
+static bool geq_r(const uint64_t (&a)[5]) {
+  if (a[4]) return true;
+  for (int i = 3; i >= 0; i--)
+    if (a[i] != RM[i]) return a[i] > RM[i];
+  return true;
+}
+static void sub_r(uint64_t (&a)[5]) {
+  uint64_t br = 0;
+  for (int i = 0; i < 4; i++) {
+    const u128 d = (u128)a[i] - RM[i] - br;
+    a[i] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1u;
+  }
+  a[4] -= br;
+}
+static uint64_t n0() {  // -r^-1 mod 2^64 (Newton)
+  uint64_t inv = 1;
+  for (int k = 0; k < 7; k++) inv *= 2 - RM[0] * inv;
+  return (uint64_t)0 - inv;
+}
+// a b 2^-256 mod r (CIOS), inputs and output < r
+static E mul(const E& a, const E& b) {
+  static const uint64_t N0 = n0();
+  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    uint64_t c = 0;
+    for (int j = 0; j < 4; j++) {
+      const u128 v = (u128)a.l[j] * b.l[i] + t[j] + c;
+      t[j] = (uint64_t)v;
+      c = (uint64_t)(v >> 64);
+    }
+    u128 v = (u128)t[4] + c;
+    t[4] = (uint64_t)v;
+    t[5] = (uint64_t)(v >> 64);
+    const uint64_t m = t[0] * N0;
+    v = (u128)m * RM[0] + t[0];
+    c = (uint64_t)(v >> 64);
+    for (int j = 1; j < 4; j++) {
+      v = (u128)m * RM[j] + t[j] + c;
+      t[j - 1] = (uint64_t)v;
+      c = (uint64_t)(v >> 64);
+    }
+    v = (u128)t[4] + c;
+    t[3] = (uint64_t)v;
+    t[4] = t[5] + (uint64_t)(v >> 64);
+  }
+  uint64_t r[5] = {t[0], t[1], t[2], t[3], t[4]};
+  if (geq_r(r)) sub_r(r);
+  return {{r[0], r[1], r[2], r[3]}};
+}
+static E add(const E& a, const E& b) {
+  uint64_t r[5];
+  uint64_t c = 0;
+  for (int i = 0; i < 4; i++) {
+    const u128 v = (u128)a.l[i] + b.l[i] + c;
+    r[i] = (uint64_t)v;
+    c = (uint64_t)(v >> 64);
+  }
+  r[4] = c;
+  if (geq_r(r)) sub_r(r);
+  return {{r[0], r[1], r[2], r[3]}};
+}
+static const E& r2() {  // 2^512 mod r: 1 doubled 512 times
+  static const E v = [] {
+    E x = {{1, 0, 0, 0}};
+    for (int k = 0; k < 512; k++) x = add(x, x);
+    return x;
+  }();
+  return v;
+}
+// the Montgomery form of the integer v (|v| < 2^63), negative values as r - |v|
+static E from_int(int64_t v) {
+  E x = {{(uint64_t)(v < 0 ? -v : v), 0, 0, 0}};
+  if (v < 0) {
+    uint64_t a[5] = {RM[0], RM[1], RM[2], RM[3], 0};
+    uint64_t br = 0;
+    for (int i = 0; i < 4; i++) {
+      const u128 d = (u128)a[i] - x.l[i] - br;
+      a[i] = (uint64_t)d;
+      br = (uint64_t)(d >> 64) & 1u;
+    }
+    x = {{a[0], a[1], a[2], a[3]}};
+  }
+  return mul(x, r2());
+}
+static E inv(const E& a) {  // a^(r - 2), Montgomery form in and out
+  uint64_t e[4] = {RM[0] - 2, RM[1], RM[2], RM[3]};
+  E acc = from_int(1);
+  for (int i = 255; i >= 0; i--) {
+    acc = mul(acc, acc);
+    if ((e[i >> 6] >> (i & 63)) & 1u) acc = mul(acc, a);
+  }
+  return acc;
+}
+}  // namespace hfr
+
+// lambda_i (plain, canonical, 8 little-endian words each) for the share indices idx[0 .. t)
+static void host_lagrange(const uint32_t* idx, size_t t, uint32_t* out) {
+  std::vector<hfr::E> num(t), den(t), pre(t + 1);
+  for (size_t i = 0; i < t; i++) {
+    const int64_t xi = (int64_t)idx[i] + 1;
+    hfr::E n = hfr::from_int(1), d = n;
+    for (size_t j = 0; j < t; j++) {
+      if (j == i) continue;
+      const int64_t xj = (int64_t)idx[j] + 1;
+      n = hfr::mul(n, hfr::from_int(xj));
+      d = hfr::mul(d, hfr::from_int(xj - xi));
+    }
+    num[i] = n;
+    den[i] = d;
+  }
+  // Montgomery's trick: one inversion for the t denominators (none is 0: the indices are distinct)
+  pre[0] = hfr::from_int(1);
+  for (size_t i = 0; i < t; i++) pre[i + 1] = hfr::mul(pre[i], den[i]);
+  hfr::E run = hfr::inv(pre[t]);
+  const hfr::E one_plain = {{1, 0, 0, 0}};
+  for (size_t i = t; i-- > 0;) {
+    const hfr::E di = hfr::mul(run, pre[i]);  // 1 / den_i
+    run = hfr::mul(run, den[i]);
+    const hfr::E lam = hfr::mul(hfr::mul(num[i], di), one_plain);  // out of Montgomery form
+    for (int w = 0; w < 4; w++) {
+      out[i * 8 + 2 * w] = (uint32_t)lam.l[w];
+      out[i * 8 + 2 * w + 1] = (uint32_t)(lam.l[w] >> 32);
+    }
+  }
+}
+
+int blsv_test_lagrange(const uint32_t* idx, size_t t, uint32_t* out) {
+  if (!idx || !out) return BLSV_EINVAL;
+  for (size_t i = 0; i < t; i++)
+    for (size_t j = 0; j < i; j++)
+      if (idx[i] == idx[j]) return BLSV_EINVAL;
+  host_lagrange(idx, t, out);
+  return BLSV_OK;
+}
+
 // Run stages 2..5 (decompress, miller, final exp, finish) on chunk [base, base + cnt) after
 // the hash stage filled H. pk_mode: 0 = group key / override entry 0, 1 = per-item table.
 struct PkSel {
@@ -449,7 +598,8 @@ int blsv_create(int device, blsv_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->spec_ev, hipEventDisableTiming);
+  for (hipEvent_t& ev : c->hash_ev)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -469,7 +619,8 @@ void blsv_destroy(blsv_ctx* c) {
     (void)hipStreamSynchronize(s);
     (void)hipStreamDestroy(s);
   }
-  if (c->spec_ev) (void)hipEventDestroy(c->spec_ev);
+  for (hipEvent_t ev : c->hash_ev)
+    if (ev) (void)hipEventDestroy(ev);
   if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
   if (c->join_ev) (void)hipEventDestroy(c->join_ev);
   (void)hipDeviceSynchronize();
@@ -900,8 +1051,9 @@ static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std:
   HIPCHK(c, c->scratch.ensure(t * 192 * 4));
   HIPCHK(c, c->out.ensure(96));
   HIPCHK(c, h2d(c, c->sel.p, sel.data(), t * 4));
-  HIPCHK(c, h2d(c, c->idx.p, idx.data(), t * 4));
-  blsk::launch_lagrange(c->idx.as<uint32_t>(), (uint32_t)t, c->lambdas.as<uint32_t>(), c->stream);
+  std::vector<uint32_t> lam(t * 8);
+  host_lagrange(idx.data(), t, lam.data());
+  HIPCHK(c, h2d(c, c->lambdas.p, lam.data(), t * 32));
   blsk::launch_lat_recover(c->S.as<uint32_t>(), cls.size(), c->s_inf.as<uint8_t>(), c->sel.as<uint32_t>(),
                            c->lambdas.as<uint32_t>(), (uint32_t)t, c->scratch.as<uint32_t>(), c->out.as<uint8_t>(),
                            c->stream);
@@ -934,10 +1086,12 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
   if (!select_shares(all_ok, index, lo, hi, t, n, sr.sel, idx)) return BLSV_OK;  // recover_from will say so
   auto& sp = c->spec[slot];
   const size_t tt = sr.sel.size();
-  // host staging: sigmas | indices | selection | 96-byte result | verify class | message, offsets, length
+  // host staging: sigmas | indices | selection | 96-byte result | verify class | message, offsets,
+  // length | Lagrange coefficients
   const size_t v_off = tt * 96 + tt * 8 + 96, m_off = v_off + 64;
   const bool verify = vmsg != nullptr && vmsg_len <= kIoCap / 4;
-  const size_t host_need = m_off + (verify ? vmsg_len + 64 : 0) + 64;
+  const size_t lam_off = (m_off + (verify ? vmsg_len + 64 : 0) + 7) & ~size_t(7);
+  const size_t host_need = lam_off + tt * 32 + 64;
   if (sp.host.sz < host_need) {  // no copy may be pending on it
     HIPCHK(c, hipStreamSynchronize(c->side));
     HIPCHK(c, hipStreamSynchronize(c->side2));
@@ -946,6 +1100,7 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
   uint8_t* h_sig = sp.host.as<uint8_t>();
   uint32_t* h_idx = reinterpret_cast<uint32_t*>(h_sig + tt * 96);
   uint32_t* h_sel = h_idx + tt;
+  uint32_t* h_lam = reinterpret_cast<uint32_t*>(h_sig + lam_off);
   for (size_t j = 0; j < tt; j++) {
     std::memcpy(h_sig + j * 96, partials + (size_t)sr.sel[j] * partial_len + 2, 96);
     h_idx[j] = idx[j];
@@ -956,28 +1111,12 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
   HIPCHK(c, sp.s_inf.ensure(tt));
   HIPCHK(c, sp.cls.ensure(tt));
   HIPCHK(c, sp.sel.ensure(tt * 4));
-  HIPCHK(c, sp.idx.ensure(tt * 4));
   HIPCHK(c, sp.lam.ensure(tt * 32));
   HIPCHK(c, sp.scratch.ensure(tt * 192 * 4));
   HIPCHK(c, sp.out.ensure(96));
-  // the Lagrange coefficients (indices only) on the second side stream beside the decoding; the
-  // interpolation waits for both
-  hipStream_t st = c->side;
-  HIPCHK(c, hipMemcpyAsync(sp.idx.p, h_idx, tt * 4, hipMemcpyHostToDevice, c->side2));
-  blsk::launch_lagrange(sp.idx.as<uint32_t>(), (uint32_t)tt, sp.lam.as<uint32_t>(), c->side2);
-  HIPCHK(c, hipEventRecord(c->spec_ev, c->side2));
-  HIPCHK(c, hipMemcpyAsync(sp.sig.p, h_sig, tt * 96, hipMemcpyHostToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(sp.sel.p, h_sel, tt * 4, hipMemcpyHostToDevice, st));
-  blsk::launch_lat_decode(sp.sig.as<uint8_t>(), 96, 0, tt, sp.S.as<uint32_t>(), sp.s_inf.as<uint8_t>(),
-                          sp.cls.as<uint8_t>(), st);
-  HIPCHK(c, hipStreamWaitEvent(st, c->spec_ev, 0));
-  blsk::launch_lat_recover(sp.S.as<uint32_t>(), tt, sp.s_inf.as<uint8_t>(), sp.sel.as<uint32_t>(),
-                           sp.lam.as<uint32_t>(), (uint32_t)tt, sp.scratch.as<uint32_t>(), sp.out.as<uint8_t>(), st);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(h_sig + tt * 96 + tt * 8, sp.out.p, 96, hipMemcpyDeviceToHost, st));
   if (verify) {
-    // VerifyRecovered(group key, msg, speculative signature) right behind the recovery on the side
-    // stream: the same latency kernel verify_messages would launch for it (kept on a hit)
+    // VerifyRecovered's message does not depend on the recovery: its hash-to-G2 starts now, on the
+    // second side stream, beside the partial verification and the recovery (wvteam.h team_hash_h)
     uint8_t* h_msg = h_sig + m_off;
     std::memcpy(h_msg, vmsg, vmsg_len);
     uint64_t* h_off = reinterpret_cast<uint64_t*>(h_msg + ((vmsg_len + 7) & ~size_t(7)));
@@ -989,13 +1128,38 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
     HIPCHK(c, sp.voff.ensure(16));
     HIPCHK(c, sp.vlen.ensure(4));
     HIPCHK(c, sp.vcls.ensure(64));
-    if (vmsg_len) HIPCHK(c, hipMemcpyAsync(sp.vmsg.p, h_msg, vmsg_len, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(sp.voff.p, h_off, 16, hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipMemcpyAsync(sp.vlen.p, h_len, 4, hipMemcpyHostToDevice, st));
+    HIPCHK(c, sp.hout.ensure(blsk::kLatHoutWords * 4));
+    HIPCHK(c, sp.saff.ensure(blsk::kLatSaffWords * 4));
+    if (vmsg_len) HIPCHK(c, hipMemcpyAsync(sp.vmsg.p, h_msg, vmsg_len, hipMemcpyHostToDevice, c->side2));
+    HIPCHK(c, hipMemcpyAsync(sp.voff.p, h_off, 16, hipMemcpyHostToDevice, c->side2));
+    HIPCHK(c, hipMemcpyAsync(sp.vlen.p, h_len, 4, hipMemcpyHostToDevice, c->side2));
+    blsk::launch_lat_hash_h(sp.vmsg.as<uint8_t>(), sp.voff.as<uint64_t>(), sp.vlen.as<uint32_t>(),
+                            sp.hout.as<uint32_t>(), c->side2);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->hash_ev[slot], c->side2));
+  }
+  // the shares' decoding first, then the Lagrange coefficients on the host (host_lagrange, ~30 us)
+  // while it runs; the interpolation follows on the same stream
+  hipStream_t st = c->side;
+  HIPCHK(c, hipMemcpyAsync(sp.sig.p, h_sig, tt * 96, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(sp.sel.p, h_sel, tt * 4, hipMemcpyHostToDevice, st));
+  blsk::launch_lat_decode(sp.sig.as<uint8_t>(), 96, 0, tt, sp.S.as<uint32_t>(), sp.s_inf.as<uint8_t>(),
+                          sp.cls.as<uint8_t>(), st);
+  host_lagrange(h_idx, tt, h_lam);
+  HIPCHK(c, hipMemcpyAsync(sp.lam.p, h_lam, tt * 32, hipMemcpyHostToDevice, st));
+  blsk::launch_lat_recover(sp.S.as<uint32_t>(), tt, sp.s_inf.as<uint8_t>(), sp.sel.as<uint32_t>(),
+                           sp.lam.as<uint32_t>(), (uint32_t)tt, sp.scratch.as<uint32_t>(), sp.out.as<uint8_t>(), st,
+                           verify ? sp.saff.as<uint32_t>() : nullptr);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(h_sig + tt * 96 + tt * 8, sp.out.p, 96, hipMemcpyDeviceToHost, st));
+  if (verify) {
+    // VerifyRecovered(group key, msg, speculative signature) right behind the recovery: the pairing
+    // check of the sum's affine point against the H hashed above (wvteam.h verify_team_pre: the
+    // class verify_messages would give the compressed bytes; kept on a hit)
+    HIPCHK(c, hipStreamWaitEvent(st, c->hash_ev[slot], 0));
     const PkSel pk = group_pk(c);
-    blsk::launch_lat_messages(sp.vmsg.as<uint8_t>(), sp.voff.as<uint64_t>(), sp.vlen.as<uint32_t>(),
-                              sp.out.as<uint8_t>(), 96, 0, 1, pk.tab, pk.inf, pk.idx, sp.vcls.as<uint8_t>(), nullptr,
-                              nullptr, st);
+    blsk::launch_lat_verify_pre(sp.hout.as<uint32_t>(), sp.saff.as<uint32_t>(), pk.tab, pk.inf,
+                                sp.vcls.as<uint8_t>(), st);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(h_sig + v_off, sp.vcls.p, 1, hipMemcpyDeviceToHost, st));
     sr.verified = true;

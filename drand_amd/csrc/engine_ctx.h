@@ -154,10 +154,11 @@ struct blsv_ctx {
   // joined back into the launch stream with these two events
   hipStream_t side = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  // the speculative recovery's Lagrange coefficients beside its decoding (blsverify.cpp
-  // spec_recover_launch): a second side stream, joined into `side` through spec_ev
+  // the speculative VerifyRecovered's hash-to-G2 of its message from the start of a threshold round
+  // (blsverify.cpp spec_recover_launch, launch_lat_hash_h): a second side stream, joined into `side`
+  // through hash_ev[slot]. Three streams in all: the boxes run 4 hardware queues per process.
   hipStream_t side2 = nullptr;
-  hipEvent_t spec_ev = nullptr;
+  hipEvent_t hash_ev[2] = {nullptr, nullptr};
   std::string err;
   // group
   bool has_group = false;
@@ -189,7 +190,8 @@ struct blsv_ctx {
   // speculative recovery beside a round's partial verification (blsverify.cpp spec_recover_*): two
   // slots (V1, V2), each with its decoded shares, Lagrange coefficients, products and output
   struct SpecSlot {
-    DBuf sig, S, s_inf, cls, sel, idx, lam, scratch, out, vmsg, voff, vlen, vcls;
+    DBuf sig, S, s_inf, cls, sel, lam, scratch, out, vmsg, voff, vlen, vcls;
+    DBuf hout, saff;  // H(msg) and the recovered signature's affine point (kernels.h kLat*Words)
     PinBuf host;  // staged sigma bytes + indices in, the 96-byte result out (async copies only)
   } spec[2];
   uint64_t spec_hits = 0, spec_misses = 0;  // speculative recoveries kept / recomputed

@@ -143,24 +143,6 @@ __global__ void __launch_bounds__(TPB) k_pubpoly_eval(const uint32_t* commits, c
 }
 
 // lambda_i = prod_{j != i} x_j / (x_j - x_i) mod r, x = idx + 1; written as plain scalars
-__global__ void __launch_bounds__(TPB) k_lagrange(const uint32_t* idx, uint32_t t, uint32_t* lambdas) {
-  size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
-  if (i >= t) return;
-  const fr xi = fr_small(idx[i] + 1u);
-  fr num = fr_small(1u), den = fr_small(1u);
-  for (uint32_t j = 0; j < t; j++) {
-    if (j == i) continue;
-    const fr xj = fr_small(idx[j] + 1u);
-    num = fr_mul(num, xj);
-    den = fr_mul(den, fr_sub(xj, xi));
-  }
-  fr lam = fr_mul(num, fr_inv(den));
-  fr one_raw = {{1, 0, 0, 0, 0, 0, 0, 0}};
-  lam = fr_mul(lam, one_raw);  // out of Montgomery form
-#pragma unroll
-  for (int w = 0; w < 8; w++) lambdas[i * 8 + w] = lam.l[w];
-}
-
 // ------------------------------------------------------------------ launchers
 void launch_decompress_g1(const uint8_t* in, size_t cnt, uint32_t* tab, uint8_t* inf, uint8_t* cls, hipStream_t st) {
   if (!cnt) return;
@@ -174,10 +156,6 @@ void launch_pubpoly_eval(const uint32_t* commits, const uint8_t* commit_inf, uin
                      out_tab, out_inf);
 }
 
-void launch_lagrange(const uint32_t* idx, uint32_t t, uint32_t* lambdas, hipStream_t st) {
-  if (!t) return;
-  hipLaunchKernelGGL(k_lagrange, dim3(grid_for(t)), dim3(TPB), 0, st, idx, t, lambdas);
-}
 
 
 }  // namespace blsk

@@ -46,8 +46,10 @@ __global__ void __launch_bounds__(64 * MUL_WAVES) k_lat_recover_mul(const uint32
 }
 
 // out96 <- compress(sum of scratch[0 .. t)): strided partial sums per wave, then a tree in LDS
+// saff (optional, wvteam.h SAFF_WORDS): the sum's affine x, y and its infinity flag, for the fused
+// round's VerifyRecovered (wvteam.h verify_team_pre) without a decompression
 __global__ void __launch_bounds__(64 * SUM_WAVES) k_lat_recover_sum(const uint32_t* scratch, uint32_t t,
-                                                                    uint8_t* out96) {
+                                                                    uint8_t* out96, uint32_t* saff) {
   __shared__ uint32_t xch[SUM_WAVES * wv::POINT_WORDS];
   wv::wv_init();
   const int w = threadIdx.x >> 6;
@@ -60,18 +62,32 @@ __global__ void __launch_bounds__(64 * SUM_WAVES) k_lat_recover_sum(const uint32
     __syncthreads();
   }
   if (w == 0) {
-    const uint32_t word = wv::g2_compress_words(acc);
+    const bool inf = wv::g2_is_inf(acc);
+    uint32_t word = wv::COMPRESSED_INF_WORD0;
     const uint32_t l = threadIdx.x;
+    if (!inf) {
+      wv::F x, y;
+      wv::g2_to_affine(acc, x, y);
+      word = wv::g2_compress_affine_words(x, y);
+      if (saff) {
+        saff[l] = x.x;
+        saff[64 + l] = y.x;
+      }
+    } else if (l != 0) {
+      word = 0;
+    }
+    if (saff) saff[128 + l] = inf ? 1u : 0u;
     if (l < 24) reinterpret_cast<uint32_t*>(out96)[l] = __builtin_bswap32(word);
   }
 }
 
 void launch_lat_recover(const uint32_t* S, size_t n_s, const uint8_t* s_inf, const uint32_t* sel,
-                        const uint32_t* lambdas, uint32_t t, uint32_t* scratch, uint8_t* out96, hipStream_t st) {
+                        const uint32_t* lambdas, uint32_t t, uint32_t* scratch, uint8_t* out96, hipStream_t st,
+                        uint32_t* saff) {
   if (!t) return;
   hipLaunchKernelGGL(k_lat_recover_mul, dim3(t), dim3(64 * MUL_WAVES), 0, st, S, n_s, s_inf, sel, lambdas, t,
                      scratch);
-  hipLaunchKernelGGL(k_lat_recover_sum, dim3(1), dim3(64 * SUM_WAVES), 0, st, scratch, t, out96);
+  hipLaunchKernelGGL(k_lat_recover_sum, dim3(1), dim3(64 * SUM_WAVES), 0, st, scratch, t, out96, saff);
 }
 
 }  // namespace blsk

@@ -85,18 +85,25 @@ void launch_decompress_g1(const uint8_t* in, size_t cnt, uint32_t* tab, uint8_t*
 // PubPoly.Eval(idx[i]) over t commits (affine table, none at infinity assumed via inf flags)
 void launch_pubpoly_eval(const uint32_t* commits, const uint8_t* commit_inf, uint32_t t, const uint32_t* idx,
                          size_t cnt, uint32_t* out_tab, uint8_t* out_inf, hipStream_t st);
-// Lagrange basis at 0 for x_i = idx[i] + 1 over Fr, written as plain 8-word little-endian scalars
 // decode only on the latency engine (k_lat.hip; one two-wave workgroup per signature)
 void launch_lat_decode(const uint8_t* sigs, size_t stride, size_t offset, size_t cnt, uint32_t* S, uint8_t* s_inf,
                        uint8_t* cls, hipStream_t st);
 void launch_decompress_g2_only(const uint8_t* sigs, size_t stride, size_t offset, size_t cnt, uint32_t* S,
                                uint8_t* s_inf, uint8_t* cls, hipStream_t st);
-void launch_lagrange(const uint32_t* idx, uint32_t t, uint32_t* lambdas, hipStream_t st);
 // sum_i [lambda_i] S_i over the selected affine staging entries sel[i] (S in SoA of stride n_s),
 // compressed to 96 bytes
 // [lambda_i] S_sel[i] summed and compressed (k_latrec.hip, lane form); scratch >= t * 192 words
+// saff (optional, k_lat.hip kLatSaffWords words): the sum's affine point for launch_lat_verify_pre
 void launch_lat_recover(const uint32_t* S, size_t n_s, const uint8_t* s_inf, const uint32_t* sel,
-                        const uint32_t* lambdas, uint32_t t, uint32_t* scratch, uint8_t* out96, hipStream_t st);
+                        const uint32_t* lambdas, uint32_t t, uint32_t* scratch, uint8_t* out96, hipStream_t st,
+                        uint32_t* saff = nullptr);
+// the fused round's VerifyRecovered in two launches (wvteam.h team_hash_h / verify_team_pre): H of
+// message 0 of (msgs, off, len) into hout, then the pairing check of the affine signature saff
+// (launch_lat_recover) against it under key pk_tab[0] -> cls[0]
+constexpr size_t kLatHoutWords = 256, kLatSaffWords = 192;
+void launch_lat_hash_h(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t* hout, hipStream_t st);
+void launch_lat_verify_pre(const uint32_t* hout, const uint32_t* saff, const uint32_t* pk_tab, const uint8_t* pk_inf,
+                           uint8_t* cls, hipStream_t st);
 // signatures: out + i*out_stride (+2 index prefix when index >= 0) = compress(sk * H(msg_i))
 void launch_sign(const uint32_t* sk_words, int32_t index, const uint32_t* H, const uint8_t* h_inf, size_t cnt,
                  uint8_t* out, size_t out_stride, hipStream_t st);

@@ -138,12 +138,10 @@ WVI G2J g2_mul_digit(const F& qx, const F& qy, uint64_t k) {
   return acc;
 }
 
-// ZCash compressed encoding of a point, as 24 big-endian words (lane j < 24 returns word j)
-WVI V g2_compress_words(const G2J& p) {
+// ZCash compressed encoding of a finite point given affine, as 24 big-endian words (lane j < 24
+// returns word j)
+WVI V g2_compress_affine_words(const F& x, const F& y) {
   const V l = lane_id();
-  if (g2_is_inf(p)) return sel(l == 0u, vsplat(0xc0000000u), vsplat(0));
-  F x, y;
-  g2_to_affine(p, x, y);
   uint32_t w0[12], w1[12];
   const V xr = raw_canon(x);
   limbs_to_words(xr, 0, w0);
@@ -158,6 +156,15 @@ WVI V g2_compress_words(const G2J& p) {
     out = sel(l == (uint32_t)(12 + j), vsplat(w0[11 - j]), out);  // x.c0
   }
   return out | sel(l == 0u, vsplat(0x80000000u | (largest ? 0x20000000u : 0u)), vsplat(0));
+}
+constexpr uint32_t COMPRESSED_INF_WORD0 = 0xc0000000u;
+
+// ZCash compressed encoding of a point, as 24 big-endian words (lane j < 24 returns word j)
+WVI V g2_compress_words(const G2J& p) {
+  if (g2_is_inf(p)) return sel(lane_id() == 0u, vsplat(COMPRESSED_INF_WORD0), vsplat(0));
+  F x, y;
+  g2_to_affine(p, x, y);
+  return g2_compress_affine_words(x, y);
 }
 
 }  // namespace wv

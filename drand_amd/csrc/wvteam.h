@@ -879,4 +879,96 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
   return one ? bls::REJ_OK : bls::REJ_PAIRING;
 }
 
+
+// ------------------------------------------------------------------ VerifyRecovered in two launches
+// The fused threshold round (blsverify.cpp spec_recover_launch) verifies the signature it recovers
+// speculatively. Its message is known from the start, so phase A's hash branch runs as its own launch
+// (team_hash_h) beside the partial verification and the recovery; the recovered signature reaches the
+// check as the affine point the interpolation computed (k_lat_recover_sum), not as bytes, so there is
+// no decompression and no subgroup check: the sum of shares whose partials all verified lies in G2,
+// and on a miss the host verifies the recomputed signature the whole way. What is left after the
+// recovery is phase B with both Miller loops at once (two teams of four waves) and phase C: the class
+// verify_team gives the compressed signature (compress -> decompress is the identity on G2).
+constexpr uint32_t KEY_TEAM = ALL_WAVES & ~SIG_TEAM;  // waves 0, 1, 4, 5: SIMDs 0 and 1
+// a hand-off buffer in global memory: Fp2 values at 64-word steps, then one flag row
+constexpr int HOUT_WORDS = 4 * 64;  // H = (X Z : Y : Z^3), finite flag at [192]
+constexpr int SAFF_WORDS = 3 * 64;  // sigma = (x, y) affine, infinity flag at [128]
+constexpr double HANDOFF_BOUND = 1.05;  // reduced dot outputs (checked on the host)
+WVI void gst_F(uint32_t* base, const F& v) {
+  WV_REQUIRE(bnd(v), HANDOFF_BOUND, "handed-off value");
+  gst(base, lane_id(), v.x);
+}
+WVI F gld_F(const uint32_t* base) { return mkF(gld(base, lane_id()), HANDOFF_BOUND); }
+WVI void gst_flag(uint32_t* base, bool v) { gst(base, lane_id(), vsplat(v ? 1u : 0u)); }
+WVI bool gld_flag(const uint32_t* base) {
+#ifdef WV_HOST
+  return base[0] != 0u;
+#else
+  return __builtin_amdgcn_readfirstlane(base[0]) != 0u;
+#endif
+}
+
+// phase A's hash branch alone (verify_team's waves 0, 4, 5 and the SSWU helper wave 3; the other
+// waves return): H(msg) in homogeneous projective form and its finite flag into hout
+WVI void team_hash_h(const uint32_t (&b0)[8], uint32_t* hout) {
+  const int w = wave_id();
+  if ((HASH_TEAM >> w) & 1u) {
+    Team th = make_team(HASH_TEAM, CTR_HASH);
+    RingCounts rc;
+    G2J q = g2_infinity();
+    if (w == 0) q = team_hash_to_curve_sum(b0, rc);
+    if (w == 5) {
+      for (int k = 0; k < SSWU_POWS; k++) ring_pow_consume(HASH_RING, bls::EXP_P_MINUS_3_DIV_4, rc);
+      iso_serve();
+    }
+    const G2J h = team_clear_cofactor(th, q);
+    if (w == 0) {
+      const bool fin = !g2_is_inf(h);
+      if (fin) {  // Jacobian (X, Y, Z) -> homogeneous (X Z : Y : Z^3), as verify_team
+        gst_F(hout, dot(h.x, h.z));
+        gst_F(hout + 64, h.y);
+        gst_F(hout + 128, dot(h.z, sqr2(h.z)));
+      }
+      gst_flag(hout + 192, fin);
+    }
+  } else if (w == 3) {
+    aff_serve();
+  }
+}
+
+// phases B and C of verify_team for a hashed message (hin, team_hash_h) and an affine signature sin
+// (x, y, infinity flag): the signature pair's Miller loop on SIG_TEAM beside the key pair's on
+// KEY_TEAM, then the product and the final exponentiation on all eight waves
+WVI uint8_t verify_team_pre(const uint32_t* hin, const uint32_t* sin, const uint32_t* pkx, const uint32_t* pky,
+                            bool pk_inf) {
+  const int w = wave_id();
+  Team all = make_team(ALL_WAVES, CTR_ALL);
+  const bool a0 = gld_flag(hin + 192) && !pk_inf, a1 = !gld_flag(sin + 128);
+  if (!a0 && !a1) return bls::REJ_OK;  // empty product = 1 (kilic Check [ext])
+  auto key_pair = [&]() {
+    return mpair_proj(g1_coord(pkx), g1_coord(pky), gld_F(hin), gld_F(hin + 64), gld_F(hin + 128));
+  };
+  auto sig_pair = [&]() { return mpair(cst(WC_NEG_G1_X), cst(WC_NEG_G1_Y), gld_F(sin), gld_F(sin + 64)); };
+  int f;
+  if (a0 && a1) {
+    // both loops run the same 68 steps, so their results sit at the same offset of their areas
+    int off;
+    if ((SIG_TEAM >> w) & 1u) {
+      Team t1 = make_team(SIG_TEAM, CTR_SIG);
+      off = team_miller(t1, sig_pair(), TB1) - TB1;
+    } else {
+      Team t0 = make_team(KEY_TEAM, CTR_HASH);
+      off = team_miller(t0, key_pair(), TB0) - TB0;
+    }
+    team_sync(all);
+    team_op(all, W_R, [&](int k) { return w12_mul_c(xld_w12(TB0 + off), xld_w12(TB1 + off), k); });
+    f = W_R;
+  } else if (a0) {
+    f = team_miller(all, key_pair(), TB0);
+  } else {
+    f = team_miller(all, sig_pair(), TB1);
+  }
+  return team_final_exp_is_one(all, f) ? bls::REJ_OK : bls::REJ_PAIRING;
+}
+
 }  // namespace wv

@@ -84,6 +84,13 @@ int blsv_profile_enable(blsv_ctx* ctx, int on);
 int blsv_lat_trace(blsv_ctx* ctx, uint64_t* ticks, int n, double* ticks_per_us, int clear);
 int blsv_lat_trace_enable(blsv_ctx* ctx, int on);
 int blsv_profile_read(blsv_ctx* ctx, double* ms, uint64_t* launches, uint64_t* items, int nstages);
+/*
+ * The Lagrange basis at 0 that blsv_recover / blsv_aggregate* interpolate with (kyber
+ * share.RecoverCommit [ext]): lambda_i = prod_{j != i} x_j / (x_j - x_i) over Fr for x_i = idx[i] + 1,
+ * written as t canonical 8-word little-endian scalars. Host arithmetic only (no device, no context):
+ * BLSV_EINVAL for repeated indices.
+ */
+int blsv_test_lagrange(const uint32_t* idx, size_t t, uint32_t* out);
 
 #ifdef __cplusplus
 }

@@ -38,6 +38,33 @@ def test_library_exports_every_symbol():
     assert b"gfx950" in lib.blsv_version()
 
 
+def test_host_lagrange_matches_integers():
+    """blsv_test_lagrange (the host Lagrange basis blsv_recover / blsv_aggregate* interpolate with,
+    blsverify.cpp host_lagrange) against Python integers: lambda_i = prod x_j / (x_j - x_i) mod r,
+    x = index + 1, for the golden round's first 33 shares, a scattered set and t = 1; repeated indices
+    are refused. No GPU: the function is host arithmetic."""
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libblsverify.so not built (run __graft_entry__.build())")
+    lib = _lib.load()
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    for idx in (list(range(33)), [65535, 0, 7, 40000, 12, 3, 999], [5]):
+        t = len(idx)
+        arr = (ctypes.c_uint32 * t)(*idx)
+        out = (ctypes.c_uint32 * (8 * t))()
+        assert lib.blsv_test_lagrange(arr, t, out) == 0
+        for i in range(t):
+            num = den = 1
+            for j in range(t):
+                if j != i:
+                    num = num * (idx[j] + 1) % R
+                    den = den * (idx[j] - idx[i]) % R
+            want = num * pow(den, R - 2, R) % R
+            got = sum(out[8 * i + w] << (32 * w) for w in range(8))
+            assert got == want, (idx, i)
+    arr = (ctypes.c_uint32 * 2)(4, 4)
+    assert lib.blsv_test_lagrange(arr, 2, (ctypes.c_uint32 * 16)()) == -1
+
+
 def test_boltload_exports_every_symbol():
     """include/boltload.h (drand.db bulk loader) against libboltload.so."""
     from drand_amd import boltdb

@@ -104,10 +104,11 @@ def test_decompress_matches_oracle(wvtest, golden):
         assert line == want, s
 
 
-@pytest.mark.parametrize("cmd", ["verify", "tverify"])
+@pytest.mark.parametrize("cmd", ["verify", "tverify", "tverify_pre"])
 def test_verify_kat_and_chain(wvtest, golden, cmd):
     """verify = one wave (wverify.h); tverify = the eight-wave team of the device kernels (wvteam.h),
-    one host thread per wave"""
+    one host thread per wave; tverify_pre = the fused round's two launches (H hashed on its own, the
+    signature handed over as an affine point: wvteam.h team_hash_h / verify_team_pre)"""
     kat = golden["kat"]
     ch = golden["chained"]
     seed = bytes.fromhex(ch["genesis_seed"])
@@ -134,6 +135,16 @@ def test_verify_mixed_golden_classes(wvtest, golden, cmd):
         prev = seed if i == 0 else sigs[i - 1]
         lines.append("%s %s %s" % (m["pk"], O.message(i + 1, prev).hex(), s.hex()))
     assert [int(x) for x in run(wvtest, cmd, lines)] == m["expect_class"]
+
+
+def test_verify_pre_infinity_signature(wvtest, golden):
+    """The split VerifyRecovered with the signature at infinity (the interpolated sum of a degenerate
+    share set): only the key pair runs, e(pk, H) != 1 rejects it -- the class verify_team gives the
+    compressed infinity, whose decoding is the point at infinity"""
+    kat = golden["kat"]
+    inf = "c0" + "00" * 95
+    line = "%s %s %s" % (kat["pk"], kat["msg"], inf)
+    assert run(wvtest, "tverify_pre", [line]) == run(wvtest, "tverify", [line]) == ["7"]
 
 
 def test_recover_four_wave_lambda_product(wvtest, golden):

@@ -185,6 +185,69 @@ static int cmd_tverify() {
   return 0;
 }
 
+// tverify_pre: as tverify, through the fused round's two launches (wvteam.h team_hash_h, then
+// verify_team_pre on the signature's affine point). The point is decoded by one wave and handed over
+// the way k_lat_recover_sum hands over the interpolated sum: Jacobian (x z^2, y z^3, z) with z = x + 1,
+// back to affine by g2_to_affine. Lines whose signature does not decode print its class (the
+// speculative path never sees such a signature: its shares all verified).
+static int cmd_tverify_pre() {
+  char a[300], b[4000], c[300];
+  static uint32_t hbuf[HOUT_WORDS], sbuf[SAFF_WORDS];
+  while (scanf("%299s %3999s %299s", a, b, c) == 3) {
+    const auto pk = unhex(a), msg = unhex(strcmp(b, "-") ? b : ""), sig = unhex(c);
+    bls::g1a P;
+    bool pinf = false;
+    if (bls::g1_decompress(pk.data(), P, pinf) != bls::REJ_OK) {
+      printf("-1\n");
+      continue;
+    }
+    if (sig.size() != 96) {
+      printf("%d\n", bls::REJ_LENGTH);
+      continue;
+    }
+    uint32_t b0[8];
+    msg_b0(msg, b0);
+    g_host_wave = 0;
+    wv_init();
+    F x, y;
+    bool sinf = false;
+    const uint8_t dc = g2_decompress(sig.data(), x, y, sinf);
+    if (dc != bls::REJ_OK) {
+      printf("%d\n", dc);
+      continue;
+    }
+    memset(sbuf, 0, sizeof sbuf);
+    if (!sinf) {
+      const F z = add(x, cst(WC_ONE2)), z2 = sqr2(z);
+      F ax, ay;
+      g2_to_affine({dot(x, z2), dot(y, dot(z2, z)), z}, ax, ay);
+      gst_F(sbuf, ax);
+      gst_F(sbuf + 64, ay);
+    }
+    gst_flag(sbuf + 128, sinf);
+    memset(hbuf, 0, sizeof hbuf);
+    for (int pass = 0; pass < 2; pass++) {
+      for (auto& ctr : g_host_ctr) ctr.store(0);
+      int cls[TEAM_WAVES];
+      std::thread th[TEAM_WAVES];
+      for (int w = 0; w < TEAM_WAVES; w++)
+        th[w] = std::thread([&, w]() {
+          g_host_wave = w;
+          wv_init();
+          if (pass == 0) team_hash_h(b0, hbuf);
+          else cls[w] = verify_team_pre(hbuf, sbuf, P.x.l, P.y.l, pinf);
+        });
+      for (auto& t : th) t.join();
+      if (pass == 0) continue;
+      for (int w = 1; w < TEAM_WAVES; w++)
+        if (cls[w] != cls[0]) fprintf(stderr, "waves disagree: %d vs %d\n", cls[w], cls[0]), abort();
+      printf("%d\n", cls[0]);
+    }
+    fflush(stdout);
+  }
+  return 0;
+}
+
 // hash: "msg" -> "inf x0 x1 y0 y1" (affine raw hex)
 static int cmd_hash() {
   char b[4000];
@@ -379,6 +442,7 @@ int main(int argc, char** argv) {
   if (argc >= 2 && !strcmp(argv[1], "teamadd")) return cmd_teamadd();
   if (argc >= 2 && !strcmp(argv[1], "verify")) return cmd_verify();
   if (argc >= 2 && !strcmp(argv[1], "tverify")) return cmd_tverify();
+  if (argc >= 2 && !strcmp(argv[1], "tverify_pre")) return cmd_tverify_pre();
   if (argc >= 2 && !strcmp(argv[1], "hash")) return cmd_hash();
   if (argc >= 2 && !strcmp(argv[1], "decompress")) return cmd_decompress();
   if (argc >= 2 && !strcmp(argv[1], "opcount")) return cmd_opcount();
