@@ -1115,8 +1115,9 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
   HIPCHK(c, sp.scratch.ensure(tt * 192 * 4));
   HIPCHK(c, sp.out.ensure(96));
   if (verify) {
-    // VerifyRecovered's message does not depend on the recovery: its hash-to-G2 starts now, on the
-    // second side stream, beside the partial verification and the recovery (wvteam.h team_hash_h)
+    // VerifyRecovered's message and key do not depend on the recovery: its hash-to-G2 and the key
+    // pair's Miller loop start now, on the second side stream, beside the partial verification and
+    // the recovery (wvteam.h team_hash_key)
     uint8_t* h_msg = h_sig + m_off;
     std::memcpy(h_msg, vmsg, vmsg_len);
     uint64_t* h_off = reinterpret_cast<uint64_t*>(h_msg + ((vmsg_len + 7) & ~size_t(7)));
@@ -1133,8 +1134,9 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
     if (vmsg_len) HIPCHK(c, hipMemcpyAsync(sp.vmsg.p, h_msg, vmsg_len, hipMemcpyHostToDevice, c->side2));
     HIPCHK(c, hipMemcpyAsync(sp.voff.p, h_off, 16, hipMemcpyHostToDevice, c->side2));
     HIPCHK(c, hipMemcpyAsync(sp.vlen.p, h_len, 4, hipMemcpyHostToDevice, c->side2));
-    blsk::launch_lat_hash_h(sp.vmsg.as<uint8_t>(), sp.voff.as<uint64_t>(), sp.vlen.as<uint32_t>(),
-                            sp.hout.as<uint32_t>(), c->side2);
+    const PkSel pk = group_pk(c);
+    blsk::launch_lat_hash_key(sp.vmsg.as<uint8_t>(), sp.voff.as<uint64_t>(), sp.vlen.as<uint32_t>(), pk.tab, pk.inf,
+                              sp.hout.as<uint32_t>(), c->side2);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->hash_ev[slot], c->side2));
   }
@@ -1153,13 +1155,12 @@ static int spec_recover_launch(blsv_ctx* c, int slot, const uint8_t* partials, s
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(h_sig + tt * 96 + tt * 8, sp.out.p, 96, hipMemcpyDeviceToHost, st));
   if (verify) {
-    // VerifyRecovered(group key, msg, speculative signature) right behind the recovery: the pairing
-    // check of the sum's affine point against the H hashed above (wvteam.h verify_team_pre: the
-    // class verify_messages would give the compressed bytes; kept on a hit)
+    // VerifyRecovered(group key, msg, speculative signature) right behind the recovery: the signature
+    // pair of the sum's affine point, the product with the key pair's Miller value computed above and
+    // the final exponentiation (wvteam.h verify_team_pre: the class verify_messages would give the
+    // compressed bytes; kept on a hit)
     HIPCHK(c, hipStreamWaitEvent(st, c->hash_ev[slot], 0));
-    const PkSel pk = group_pk(c);
-    blsk::launch_lat_verify_pre(sp.hout.as<uint32_t>(), sp.saff.as<uint32_t>(), pk.tab, pk.inf,
-                                sp.vcls.as<uint8_t>(), st);
+    blsk::launch_lat_verify_pre(sp.hout.as<uint32_t>(), sp.saff.as<uint32_t>(), sp.vcls.as<uint8_t>(), st);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(h_sig + v_off, sp.vcls.p, 1, hipMemcpyDeviceToHost, st));
     sr.verified = true;

@@ -155,7 +155,7 @@ struct blsv_ctx {
   hipStream_t side = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   // the speculative VerifyRecovered's hash-to-G2 of its message from the start of a threshold round
-  // (blsverify.cpp spec_recover_launch, launch_lat_hash_h): a second side stream, joined into `side`
+  // (blsverify.cpp spec_recover_launch, launch_lat_hash_key): a second side stream, joined into `side`
   // through hash_ev[slot]. Three streams in all: the boxes run 4 hardware queues per process.
   hipStream_t side2 = nullptr;
   hipEvent_t hash_ev[2] = {nullptr, nullptr};

@@ -132,33 +132,34 @@ void launch_lat_decode(const uint8_t* sigs, size_t stride, size_t offset, size_t
   hipLaunchKernelGGL(k_lat_decode, dim3((unsigned)cnt), dim3(128), 0, st, sigs, stride, offset, cnt, S, s_inf, cls);
 }
 
-// the fused round's VerifyRecovered (blsverify.cpp spec_recover_launch): H(msg) from the start of the
-// round, then the check against the recovered signature's affine point (wvteam.h)
+// the fused round's VerifyRecovered (blsverify.cpp spec_recover_launch): H(msg) and the key pair's
+// Miller loop from the start of the round, then the rest of the check against the recovered
+// signature's affine point (wvteam.h team_hash_key / verify_team_pre)
 static_assert(kLatHoutWords == (size_t)wv::HOUT_WORDS && kLatSaffWords == (size_t)wv::SAFF_WORDS, "hand-off sizes");
-__global__ void __launch_bounds__(64 * WV_WAVES) k_lat_hash_h(const uint8_t* msgs, const uint64_t* off,
-                                                             const uint32_t* len, uint32_t* hout) {
+__global__ void __launch_bounds__(64 * WV_WAVES) k_lat_hash_key(const uint8_t* msgs, const uint64_t* off,
+                                                               const uint32_t* len, const uint32_t* pk_tab,
+                                                               const uint8_t* pk_inf, uint32_t* hout) {
   wv::team_init();
   wv::wv_init();
   __syncthreads();
   uint32_t b0[8];
   xmd_b0_bytes<true>(b0, msgs + off[0], len[0], c_lat_dst);
-  wv::team_hash_h(b0, hout);
+  wv::team_hash_key(b0, pk_tab, pk_tab + 12, pk_inf[0] != 0, hout);
 }
 __global__ void __launch_bounds__(64 * WV_WAVES) k_lat_verify_pre(const uint32_t* hout, const uint32_t* saff,
-                                                                 const uint32_t* pk_tab, const uint8_t* pk_inf,
                                                                  uint8_t* cls) {
   wv::team_init();
   wv::wv_init();
   __syncthreads();
-  const uint8_t c = wv::verify_team_pre(hout, saff, pk_tab, pk_tab + 12, pk_inf[0] != 0);
+  const uint8_t c = wv::verify_team_pre(hout, saff);
   if (threadIdx.x == 0) cls[0] = c;
 }
-void launch_lat_hash_h(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t* hout, hipStream_t st) {
-  hipLaunchKernelGGL(k_lat_hash_h, dim3(1), dim3(64 * WV_WAVES), 0, st, msgs, off, len, hout);
+void launch_lat_hash_key(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, const uint32_t* pk_tab,
+                         const uint8_t* pk_inf, uint32_t* hout, hipStream_t st) {
+  hipLaunchKernelGGL(k_lat_hash_key, dim3(1), dim3(64 * WV_WAVES), 0, st, msgs, off, len, pk_tab, pk_inf, hout);
 }
-void launch_lat_verify_pre(const uint32_t* hout, const uint32_t* saff, const uint32_t* pk_tab, const uint8_t* pk_inf,
-                           uint8_t* cls, hipStream_t st) {
-  hipLaunchKernelGGL(k_lat_verify_pre, dim3(1), dim3(64 * WV_WAVES), 0, st, hout, saff, pk_tab, pk_inf, cls);
+void launch_lat_verify_pre(const uint32_t* hout, const uint32_t* saff, uint8_t* cls, hipStream_t st) {
+  hipLaunchKernelGGL(k_lat_verify_pre, dim3(1), dim3(64 * WV_WAVES), 0, st, hout, saff, cls);
 }
 
 // the phase marks of the last latency launch's item 0 (wteam.h WV_MARK), device wall-clock ticks

@@ -97,13 +97,13 @@ void launch_decompress_g2_only(const uint8_t* sigs, size_t stride, size_t offset
 void launch_lat_recover(const uint32_t* S, size_t n_s, const uint8_t* s_inf, const uint32_t* sel,
                         const uint32_t* lambdas, uint32_t t, uint32_t* scratch, uint8_t* out96, hipStream_t st,
                         uint32_t* saff = nullptr);
-// the fused round's VerifyRecovered in two launches (wvteam.h team_hash_h / verify_team_pre): H of
-// message 0 of (msgs, off, len) into hout, then the pairing check of the affine signature saff
-// (launch_lat_recover) against it under key pk_tab[0] -> cls[0]
-constexpr size_t kLatHoutWords = 256, kLatSaffWords = 192;
-void launch_lat_hash_h(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, uint32_t* hout, hipStream_t st);
-void launch_lat_verify_pre(const uint32_t* hout, const uint32_t* saff, const uint32_t* pk_tab, const uint8_t* pk_inf,
-                           uint8_t* cls, hipStream_t st);
+// the fused round's VerifyRecovered in two launches (wvteam.h team_hash_key / verify_team_pre): H of
+// message 0 of (msgs, off, len) and the Miller loop of (pk_tab[0], H) into hout, then the pairing
+// check of the affine signature saff (launch_lat_recover) against it -> cls[0]
+constexpr size_t kLatHoutWords = 448, kLatSaffWords = 192;
+void launch_lat_hash_key(const uint8_t* msgs, const uint64_t* off, const uint32_t* len, const uint32_t* pk_tab,
+                         const uint8_t* pk_inf, uint32_t* hout, hipStream_t st);
+void launch_lat_verify_pre(const uint32_t* hout, const uint32_t* saff, uint8_t* cls, hipStream_t st);
 // signatures: out + i*out_stride (+2 index prefix when index >= 0) = compress(sk * H(msg_i))
 void launch_sign(const uint32_t* sk_words, int32_t index, const uint32_t* H, const uint8_t* h_inf, size_t cnt,
                  uint8_t* out, size_t out_stride, hipStream_t st);

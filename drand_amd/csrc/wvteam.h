@@ -882,16 +882,16 @@ WVI uint8_t verify_team(const uint8_t* sig, const uint32_t (&b0)[8], const uint3
 
 // ------------------------------------------------------------------ VerifyRecovered in two launches
 // The fused threshold round (blsverify.cpp spec_recover_launch) verifies the signature it recovers
-// speculatively. Its message is known from the start, so phase A's hash branch runs as its own launch
-// (team_hash_h) beside the partial verification and the recovery; the recovered signature reaches the
-// check as the affine point the interpolation computed (k_lat_recover_sum), not as bytes, so there is
-// no decompression and no subgroup check: the sum of shares whose partials all verified lies in G2,
-// and on a miss the host verifies the recomputed signature the whole way. What is left after the
-// recovery is phase B with both Miller loops at once (two teams of four waves) and phase C: the class
+// speculatively. Its message and the group key are known from the start, so phase A's hash branch
+// and then phase B's key-pair Miller loop run as their own launch (team_hash_key) beside the partial
+// verification and the recovery; the recovered signature reaches the check as the affine point the
+// interpolation computed (k_lat_recover_sum), not as bytes, so there is no decompression and no
+// subgroup check: the sum of shares whose partials all verified lies in G2, and on a miss the host
+// verifies the recomputed signature the whole way. What is left after the recovery is the signature
+// pair's Miller loop on all eight waves, the product and phase C (verify_team_pre): the class
 // verify_team gives the compressed signature (compress -> decompress is the identity on G2).
-constexpr uint32_t KEY_TEAM = ALL_WAVES & ~SIG_TEAM;  // waves 0, 1, 4, 5: SIMDs 0 and 1
-// a hand-off buffer in global memory: Fp2 values at 64-word steps, then one flag row
-constexpr int HOUT_WORDS = 4 * 64;  // H = (X Z : Y : Z^3), finite flag at [192]
+// a hand-off buffer in global memory: Fp values at 64-word steps, then one flag row
+constexpr int HOUT_WORDS = 7 * 64;  // the key pair's Miller value f0 (6 coefficients), its active flag at [384]
 constexpr int SAFF_WORDS = 3 * 64;  // sigma = (x, y) affine, infinity flag at [128]
 constexpr double HANDOFF_BOUND = 1.05;  // reduced dot outputs (checked on the host)
 WVI void gst_F(uint32_t* base, const F& v) {
@@ -899,6 +899,11 @@ WVI void gst_F(uint32_t* base, const F& v) {
   gst(base, lane_id(), v.x);
 }
 WVI F gld_F(const uint32_t* base) { return mkF(gld(base, lane_id()), HANDOFF_BOUND); }
+WVI W12 gld_w12(const uint32_t* base) {
+  W12 r;
+  for (int k = 0; k < 6; k++) r.c[k] = gld_F(base + 64 * k);
+  return r;
+}
 WVI void gst_flag(uint32_t* base, bool v) { gst(base, lane_id(), vsplat(v ? 1u : 0u)); }
 WVI bool gld_flag(const uint32_t* base) {
 #ifdef WV_HOST
@@ -908,10 +913,12 @@ WVI bool gld_flag(const uint32_t* base) {
 #endif
 }
 
-// phase A's hash branch alone (verify_team's waves 0, 4, 5 and the SSWU helper wave 3; the other
-// waves return): H(msg) in homogeneous projective form and its finite flag into hout
-WVI void team_hash_h(const uint32_t (&b0)[8], uint32_t* hout) {
+// phase A's hash branch (verify_team's waves 0, 4, 5 and the SSWU helper wave 3), then phase B's key
+// pair e(pk, H) on all eight waves: its Miller value and whether the pair is active into hout
+WVI void team_hash_key(const uint32_t (&b0)[8], const uint32_t* pkx, const uint32_t* pky, bool pk_inf,
+                       uint32_t* hout) {
   const int w = wave_id();
+  Team all = make_team(ALL_WAVES, CTR_ALL);
   if ((HASH_TEAM >> w) & 1u) {
     Team th = make_team(HASH_TEAM, CTR_HASH);
     RingCounts rc;
@@ -925,48 +932,44 @@ WVI void team_hash_h(const uint32_t (&b0)[8], uint32_t* hout) {
     if (w == 0) {
       const bool fin = !g2_is_inf(h);
       if (fin) {  // Jacobian (X, Y, Z) -> homogeneous (X Z : Y : Z^3), as verify_team
-        gst_F(hout, dot(h.x, h.z));
-        gst_F(hout + 64, h.y);
-        gst_F(hout + 128, dot(h.z, sqr2(h.z)));
+        xst(S_HX, dot(h.x, h.z));
+        xst(S_HY, h.y);
+        xst(S_HZ, dot(h.z, sqr2(h.z)));
       }
-      gst_flag(hout + 192, fin);
+      xst_word(XW_HFIN, fin);
     }
   } else if (w == 3) {
     aff_serve();
   }
+  team_sync(all);
+  const bool a0 = xld_word(XW_HFIN) && !pk_inf;
+  if (a0) {
+    const MPair m0 = mpair_proj(g1_coord(pkx), g1_coord(pky), xld(S_HX), xld(S_HY), xld(S_HZ));
+    const int f = team_miller(all, m0, TB0);
+    for (int k = all.id; k < 6; k += all.n) gst_F(hout + 64 * k, xld(f + k));
+  }
+  if (w == 0) gst_flag(hout + 384, a0);
 }
 
-// phases B and C of verify_team for a hashed message (hin, team_hash_h) and an affine signature sin
-// (x, y, infinity flag): the signature pair's Miller loop on SIG_TEAM beside the key pair's on
-// KEY_TEAM, then the product and the final exponentiation on all eight waves
-WVI uint8_t verify_team_pre(const uint32_t* hin, const uint32_t* sin, const uint32_t* pkx, const uint32_t* pky,
-                            bool pk_inf) {
-  const int w = wave_id();
+// phases B and C of verify_team after team_hash_key (hin) for an affine signature sin (x, y,
+// infinity flag): the signature pair's Miller loop on all eight waves, the product with the key
+// pair's value and the final exponentiation
+WVI uint8_t verify_team_pre(const uint32_t* hin, const uint32_t* sin) {
   Team all = make_team(ALL_WAVES, CTR_ALL);
-  const bool a0 = gld_flag(hin + 192) && !pk_inf, a1 = !gld_flag(sin + 128);
+  const bool a0 = gld_flag(hin + 384), a1 = !gld_flag(sin + 128);
   if (!a0 && !a1) return bls::REJ_OK;  // empty product = 1 (kilic Check [ext])
-  auto key_pair = [&]() {
-    return mpair_proj(g1_coord(pkx), g1_coord(pky), gld_F(hin), gld_F(hin + 64), gld_F(hin + 128));
-  };
-  auto sig_pair = [&]() { return mpair(cst(WC_NEG_G1_X), cst(WC_NEG_G1_Y), gld_F(sin), gld_F(sin + 64)); };
   int f;
-  if (a0 && a1) {
-    // both loops run the same 68 steps, so their results sit at the same offset of their areas
-    int off;
-    if ((SIG_TEAM >> w) & 1u) {
-      Team t1 = make_team(SIG_TEAM, CTR_SIG);
-      off = team_miller(t1, sig_pair(), TB1) - TB1;
-    } else {
-      Team t0 = make_team(KEY_TEAM, CTR_HASH);
-      off = team_miller(t0, key_pair(), TB0) - TB0;
+  if (a1) {
+    const MPair m1 = mpair(cst(WC_NEG_G1_X), cst(WC_NEG_G1_Y), gld_F(sin), gld_F(sin + 64));
+    const int f1 = team_miller(all, m1, TB1);
+    f = f1;
+    if (a0) {
+      team_op(all, W_R, [&](int k) { return w12_mul_c(gld_w12(hin), xld_w12(f1), k); });
+      f = W_R;
     }
-    team_sync(all);
-    team_op(all, W_R, [&](int k) { return w12_mul_c(xld_w12(TB0 + off), xld_w12(TB1 + off), k); });
-    f = W_R;
-  } else if (a0) {
-    f = team_miller(all, key_pair(), TB0);
   } else {
-    f = team_miller(all, sig_pair(), TB1);
+    team_op(all, W_R, [&](int k) { return gld_F(hin + 64 * k); });
+    f = W_R;
   }
   return team_final_exp_is_one(all, f) ? bls::REJ_OK : bls::REJ_PAIRING;
 }

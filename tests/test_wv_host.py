@@ -108,7 +108,7 @@ def test_decompress_matches_oracle(wvtest, golden):
 def test_verify_kat_and_chain(wvtest, golden, cmd):
     """verify = one wave (wverify.h); tverify = the eight-wave team of the device kernels (wvteam.h),
     one host thread per wave; tverify_pre = the fused round's two launches (H hashed on its own, the
-    signature handed over as an affine point: wvteam.h team_hash_h / verify_team_pre)"""
+    signature handed over as an affine point: wvteam.h team_hash_key / verify_team_pre)"""
     kat = golden["kat"]
     ch = golden["chained"]
     seed = bytes.fromhex(ch["genesis_seed"])
@@ -140,11 +140,16 @@ def test_verify_mixed_golden_classes(wvtest, golden, cmd):
 def test_verify_pre_infinity_signature(wvtest, golden):
     """The split VerifyRecovered with the signature at infinity (the interpolated sum of a degenerate
     share set): only the key pair runs, e(pk, H) != 1 rejects it -- the class verify_team gives the
-    compressed infinity, whose decoding is the point at infinity"""
+    compressed infinity, whose decoding is the point at infinity. And with the key at infinity: the
+    signature pair alone (rejected), or no pair at all (the empty product accepts, as kilic's Check)"""
     kat = golden["kat"]
     inf = "c0" + "00" * 95
     line = "%s %s %s" % (kat["pk"], kat["msg"], inf)
     assert run(wvtest, "tverify_pre", [line]) == run(wvtest, "tverify", [line]) == ["7"]
+    # the key at infinity (the key pair inactive): the signature pair alone, and both inactive
+    pk_inf = "c0" + "00" * 47
+    lines = ["%s %s %s" % (pk_inf, kat["msg"], kat["sig"]), "%s %s %s" % (pk_inf, kat["msg"], inf)]
+    assert run(wvtest, "tverify_pre", lines) == run(wvtest, "tverify", lines) == ["7", "0"]
 
 
 def test_recover_four_wave_lambda_product(wvtest, golden):

@@ -185,7 +185,7 @@ static int cmd_tverify() {
   return 0;
 }
 
-// tverify_pre: as tverify, through the fused round's two launches (wvteam.h team_hash_h, then
+// tverify_pre: as tverify, through the fused round's two launches (wvteam.h team_hash_key, then
 // verify_team_pre on the signature's affine point). The point is decoded by one wave and handed over
 // the way k_lat_recover_sum hands over the interpolated sum: Jacobian (x z^2, y z^3, z) with z = x + 1,
 // back to affine by g2_to_affine. Lines whose signature does not decode print its class (the
@@ -234,8 +234,8 @@ static int cmd_tverify_pre() {
         th[w] = std::thread([&, w]() {
           g_host_wave = w;
           wv_init();
-          if (pass == 0) team_hash_h(b0, hbuf);
-          else cls[w] = verify_team_pre(hbuf, sbuf, P.x.l, P.y.l, pinf);
+          if (pass == 0) team_hash_key(b0, P.x.l, P.y.l, pinf, hbuf);
+          else cls[w] = verify_team_pre(hbuf, sbuf);
         });
       for (auto& t : th) t.join();
       if (pass == 0) continue;
