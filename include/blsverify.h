@@ -28,11 +28,12 @@
  * VerifyPartial, chain/beacon/node.go:112,125; identity checks, key/keys.go:60-63)
  *  - A call with at most lat_max items (blsv_set_lat_max, default 1536) runs on the LATENCY path: one
  *    workgroup of eight waves per item, every limb of a field element in its own lane
- *    (drand_amd/csrc/k_lat.hip). Measured on MI355X (profiles/r05zb_latency.json, warm): one
+ *    (drand_amd/csrc/k_lat.hip). Measured on MI355X (profiles/r06e_latency.json, warm): one
  *    VerifyRecovered 1.9 ms; blsv_aggregate of an n = 64 / t = 33 round (64 VerifyPartial +
- *    Recover + VerifyRecovered) 3.4 ms (the recovery and its verification of the shares
- *    the round would select if all verify runs beside the partial verification and is kept when
- *    the verdicts confirm that selection). Up to 256 items the time stays ~2.1 ms (every item has its
+ *    Recover + VerifyRecovered) 2.2 ms, blsv_aggregate_round V1 + V2 4.4 ms (the recovery and the
+ *    verification of the shares the round would select if all verify run beside the partial
+ *    verification -- H(msg) and the key pair's Miller loop from the start -- and are kept when the
+ *    verdicts confirm that selection). Up to 256 items the time stays ~2.1 ms (every item has its
  *    own CU), then grows ~1.9 ms per further 256 items (profiles/r05za_latency_sweep.json).
  *  - Larger calls run on the BATCH pipeline (one lane per item, staged kernels): ~14 ms floor
  *    (14.1 ms at 64 items, 15.3 ms at 2,048: profiles/r05za_latency_sweep.json), then ~0.43 us per
