@@ -14,6 +14,7 @@
 #   cabi             tools/cabi_smoke (latency contract from plain C)
 #   pmccal           FETCH_SIZE / WRITE_SIZE of tools/pmccal (known bytes in the engine's SoA patterns)
 #   wvbench          tools/wvbench (per-operation latency of the latency engine's primitives)
+#   fpbench          tools/fpbench (Fp multiply throughput: radix-2^28 interleaved vs 13 x 30-bit SOS)
 #   intrate          tools/intrate (peak v_mad_u64_u32 rate) and its SQ/GRBM counters (clock of the peak)
 #   lat              tools/latency_bench.py (lone verify, fused round)
 #   latsweep         the same with the latency-vs-batch sweep (64 .. 2048 items: co-resident teams)
@@ -73,6 +74,7 @@ for step in "$@"; do
         > "$O/pmccal_fetch.log" 2>&1 &&
       timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmccal_write" -o run -- tools/pmccal \
         > "$O/pmccal_write.log" 2>&1 || rc=24 ;;
+    fpbench) timeout -k 10 180 tools/fpbench > "$O/fpbench.json" 2>&1 || rc=28 ;;
     cabi) timeout -k 10 120 tools/cabi_smoke > "$O/cabi_smoke.txt" 2>&1 || rc=20 ;;
     wvbench) timeout -k 10 120 tools/wvbench > "$O/wvbench.json" 2>&1 || rc=25 ;;
     lat) timeout -k 10 300 python -u tools/latency_bench.py --reps 10 --out "$O/latency.json" > "$O/latency.log" 2>&1 || rc=21 ;;
