@@ -82,3 +82,107 @@ def test_verify_random_corruptions_equal_oracle(engine, golden, C, route):
     assert res.ok == [c == 0 for c in want]
     fb = next((i for i, c in enumerate(want) if c), None)
     assert res.first_bad == fb
+
+
+def _mangle_shares(rng, parts, n):
+    """Random corruptions of a round's shares: a flipped signature bit, a wrong share index, a
+    duplicate of another share (the dedup rule), a truncated-to-garbage signature."""
+    parts = list(parts)
+    for j in rng.sample(range(len(parts)), min(len(parts), rng.choice([0, 0, 1, 2, 5, 12, 30]))):
+        p = bytearray(parts[j])
+        kind = rng.randrange(4)
+        if kind == 0:
+            p[2 + rng.randrange(96)] ^= 1 << rng.randrange(8)
+        elif kind == 1:
+            idx = ((p[0] << 8 | p[1]) + 1 + rng.randrange(n - 1)) % n
+            p[0], p[1] = idx >> 8, idx & 0xFF
+        elif kind == 2:
+            p = bytearray(parts[rng.randrange(len(parts))])
+        else:
+            p[2:] = bytes(96)
+            p[2] = 0x80
+        parts[j] = bytes(p)
+    return parts
+
+
+def test_aggregate_random_rounds_equal_oracle(engine, golden, C):
+    """blsv_aggregate (VerifyPartial x k, Recover from the first t valid shares, VerifyRecovered) on
+    random share sets of the golden n=64 / t=33 round -- shuffled, between t - 2 and 64 shares, some
+    corrupted -- against the oracle's verdicts and Recover: the classes, the group signature bytes,
+    the group verdict, "not enough shares" as an error; both the speculative recovery's hits and its
+    misses are reached (spec_stats)."""
+    from drand_amd.engine import EngineError
+
+    th = golden["threshold"]
+    t, n = th["t"], th["n"]
+    commits = [bytes.fromhex(c) for c in th["commits"]]
+    msg = bytes.fromhex(th["msg"])
+    engine.set_group(commits, n)
+    grp = C.Group(commits)
+    rng = random.Random(0xA66)
+    h0, m0 = engine.spec_stats()
+    rounds = fails = 0
+    for _ in range(14):
+        parts = [bytes.fromhex(p) for p in th["partials"]]
+        rng.shuffle(parts)
+        parts = _mangle_shares(rng, parts[:rng.randrange(t - 2, n + 1)], n)
+        want_cls = [grp.verify_partial(msg, p) for p in parts]
+        want_sig = grp.recover(msg, parts, t, n)
+        if want_sig is None:
+            with pytest.raises(EngineError):
+                engine.aggregate(msg, parts, t, n)
+            fails += 1
+            continue
+        ok, cls, sig, gok = engine.aggregate(msg, parts, t, n)
+        assert cls == want_cls
+        assert ok == [c == 0 for c in want_cls]
+        assert sig == want_sig
+        assert gok == (C.verify(commits[0], msg, sig) == 0)
+        rounds += 1
+    h1, m1 = engine.spec_stats()
+    print(f"{rounds} rounds recovered, {fails} short; speculation hits {h1 - h0}, misses {m1 - m0}")
+    assert rounds >= 5 and fails >= 2 and h1 > h0 and m1 > m0
+
+
+def test_aggregate_round_v1_v2_random_equal_oracle(engine, golden, C):
+    """blsv_aggregate_round (chain/beacon/chain.go:131-166: V1 and V2 partials verified in one pass,
+    both Recovers, both group verifications) on random V1 / V2 share sets: the status follows the
+    oracle (V1 recover failure, V2 recover failure blocking the beacon, OK, OK_V2 with v2_valid), and
+    the verdicts and both signatures equal the oracle's."""
+    from drand_amd import _lib
+
+    th = golden["threshold"]
+    t, n = th["t"], th["n"]
+    commits = [bytes.fromhex(c) for c in th["commits"]]
+    msg1, msg2 = bytes.fromhex(th["msg"]), bytes.fromhex(th["msg_v2"])
+    engine.set_group(commits, n)
+    grp = C.Group(commits)
+    rng = random.Random(0xB22)
+    seen = set()
+    for _ in range(12):
+        p1 = [bytes.fromhex(p) for p in th["partials"]]
+        p2 = [bytes.fromhex(p) for p in th["partials_v2"]]
+        rng.shuffle(p1)
+        rng.shuffle(p2)
+        p1 = _mangle_shares(rng, p1[:rng.randrange(t - 1, n + 1)], n)
+        p2 = _mangle_shares(rng, p2[:rng.choice([0, t - 1, t, rng.randrange(t, n + 1)])], n)
+        st, ok1, ok2, sig1, sig2, v2 = engine.aggregate_round(msg1, p1, msg2, p2, t, n)
+        assert ok1 == [grp.verify_partial(msg1, p) == 0 for p in p1]
+        assert ok2 == [grp.verify_partial(msg2, p) == 0 for p in p2]
+        w1 = grp.recover(msg1, p1, t, n)
+        if w1 is None:
+            assert st == _lib.AGG_V1_RECOVER_FAIL
+        elif C.verify(commits[0], msg1, w1) != 0:
+            assert st == _lib.AGG_V1_INVALID and sig1 == w1
+        elif len(p2) >= t:
+            w2 = grp.recover(msg2, p2, t, n)
+            if w2 is None:
+                assert st == _lib.AGG_V2_RECOVER_FAIL and sig1 == w1
+            else:
+                assert st == _lib.AGG_OK_V2 and sig1 == w1 and sig2 == w2
+                assert v2 == (C.verify(commits[0], msg2, w2) == 0)
+        else:
+            assert st == _lib.AGG_OK and sig1 == w1 and sig2 is None
+        seen.add(st)
+    print("statuses:", sorted(seen))
+    assert len(seen) >= 3
