@@ -186,3 +186,50 @@ def test_aggregate_round_v1_v2_random_equal_oracle(engine, golden, C):
         seen.add(st)
     print("statuses:", sorted(seen))
     assert len(seen) >= 3
+
+
+def test_chained_random_kinds_single_lane_f_pass(engine, golden, C):
+    """A 70,003-round device-generated chained history (above the 3-lane f pass's 64 Ki limit, so the
+    single-lane Miller f pass and the batch pipeline verify it) with 48 rounds corrupted by random
+    kinds (_corrupt): exactly the corrupted rounds and their successors in the same 64-round segment
+    reject, first_bad is the smallest, and the class of every rejected round equals the C oracle's
+    on its own message (chain.Message of its round and the stored previous signature)."""
+    import hashlib
+
+    import torch
+
+    from test_gpu_scale import _history, _verify, NONE
+
+    n, seg = 70003, 64
+    seeds, sigs, s0 = _history(engine, golden, n, seg, seed=23)
+    host = bytearray(sigs.cpu().numpy().tobytes())
+    orig = bytes(host)
+    rng = random.Random(0xC4A1)
+    bad = sorted(rng.sample(range(n), 48))
+    view = [orig[i * 96:(i + 1) * 96] for i in range(n)]
+    for i in bad:
+        host[i * 96:(i + 1) * 96] = _corrupt(rng, view, i)
+    sigs.copy_(torch.frombuffer(bytearray(host), dtype=torch.uint8).to("cuda:0"))
+    prev = engine.set_lat_max(0)
+    try:
+        ok, fb, cls = _verify(engine, 1, seg, seeds, s0, sigs, n)
+    finally:
+        engine.set_lat_max(prev)
+    sd = seeds.cpu().numpy().tobytes()
+    pk = bytes.fromhex(golden["chained"]["pk"])
+
+    def prev_of(i):
+        if i % seg == 0:
+            s = i // seg
+            return sd[s * 96: s * 96 + (s0 if s == 0 else 96)]
+        return bytes(host[(i - 1) * 96: i * 96])
+
+    cand = sorted(set(bad) | {i + 1 for i in bad if i + 1 < n and (i + 1) % seg})
+    want = {}
+    for i in cand:
+        msg = hashlib.sha256(prev_of(i) + (i + 1).to_bytes(8, "big")).digest()
+        want[i] = C.verify(pk, msg, bytes(host[i * 96:(i + 1) * 96]))
+    rejected = {i for i, v in enumerate(ok) if not v}
+    assert rejected == {i for i, c in want.items() if c}
+    assert all(cls[i] == want[i] for i in cand)
+    assert fb == (1 + min(rejected) if rejected else NONE)
