@@ -510,6 +510,8 @@ static int decode_g1(blsv_ctx* c, const uint8_t* pk48, size_t cnt, DBuf& tab, DB
 static int upload_messages(blsv_ctx* c, const uint8_t* msgs, const uint32_t* msg_lens, size_t n) {
   std::vector<uint64_t> off(n + 1, 0);
   for (size_t i = 0; i < n; i++) off[i + 1] = off[i] + msg_lens[i];
+  if (off[n] && !msgs) return fail(c, BLSV_EINVAL, "messages: %llu message bytes but no buffer",
+                                   (unsigned long long)off[n]);
   HIPCHK(c, c->in_msgs.ensure(off[n] + 1));
   HIPCHK(c, c->in_off.ensure((n + 1) * 8));
   HIPCHK(c, c->in_len.ensure(n * 4 + 4));
@@ -670,6 +672,7 @@ int blsv_verify_chained(blsv_ctx* c, uint64_t first_round, const uint8_t* prev0,
   if (!c->has_group) return fail(c, BLSV_ENOGROUP, "verify_chained: no group key set");
   if (n && (!sigs96 || !prev0 || (prev0_len != 32 && prev0_len != 96)))
     return fail(c, BLSV_EINVAL, "verify_chained: prev0 must be 32 or 96 bytes");
+  if (n > SIZE_MAX / 96 - 1) return fail(c, BLSV_EINVAL, "verify_chained: %zu rounds overflow the byte count", n);
   (void)hipSetDevice(c->device);
   HIPCHK(c, c->in_sigs.ensure(n * 96 + 96));
   HIPCHK(c, c->seeds.ensure(96));

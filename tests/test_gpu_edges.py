@@ -169,3 +169,25 @@ def test_verify_partials_multi_rounds(engine, golden):
     # agrees with the single-message entry point round by round
     for i in (0, 9, 23):
         assert engine.verify_partials(msgs[i], [parts[i]])[0] == [True]
+
+
+@pytest.mark.gpu
+def test_verify_messages_null_message_buffer(engine, golden):
+    """A message length without a message buffer is refused (BLSV_EINVAL), not dereferenced; zero-length
+    messages need no buffer."""
+    import ctypes
+
+    from drand_amd import _lib
+
+    kat = golden["kat"]
+    sig = bytes.fromhex(kat["sig"])
+    lens = (ctypes.c_uint32 * 1)(5)
+    bm, cls = _lib.out_buf(1), _lib.out_buf(1)
+    fb = ctypes.c_uint64()
+    rc = engine.lib.blsv_verify_messages(engine._h, _lib.buf(bytes.fromhex(kat["pk"])), None, lens, 1, _lib.buf(sig),
+                                         bm, ctypes.byref(fb), cls)
+    assert rc == -1
+    lens[0] = 0
+    rc = engine.lib.blsv_verify_messages(engine._h, _lib.buf(bytes.fromhex(kat["pk"])), None, lens, 1, _lib.buf(sig),
+                                         bm, ctypes.byref(fb), cls)
+    assert rc == 0 and cls[0] == 7  # the KAT signature over the empty message fails the pairing
