@@ -975,7 +975,7 @@ static int partials_stage(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const
 int blsv_verify_partials(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
                          size_t k, uint8_t* ok, uint8_t* reject_class) {
   if (!c) return BLSV_EINVAL;
-  if (k && (!partials || !ok)) return fail(c, BLSV_EINVAL, "verify_partials: null arguments");
+  if ((k && (!partials || !ok)) || (msg_len && !msg)) return fail(c, BLSV_EINVAL, "verify_partials: null arguments");
   (void)hipSetDevice(c->device);
   std::vector<uint8_t> cls;
   std::vector<uint32_t> index;
@@ -1010,7 +1010,7 @@ static int recover_from(blsv_ctx* c, const std::vector<uint8_t>& cls, const std:
 int blsv_recover(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_t* partials, size_t partial_len,
                  size_t k, size_t t, size_t n, uint8_t* out_sig96) {
   if (!c) return BLSV_EINVAL;
-  if (!out_sig96 || t == 0 || (k && !partials)) return fail(c, BLSV_EINVAL, "recover: bad arguments");
+  if (!out_sig96 || t == 0 || (k && !partials) || (msg_len && !msg)) return fail(c, BLSV_EINVAL, "recover: bad arguments");
   (void)hipSetDevice(c->device);
   std::vector<uint8_t> cls;
   std::vector<uint32_t> index;
@@ -1222,7 +1222,7 @@ int blsv_aggregate(blsv_ctx* c, const uint8_t* msg, size_t msg_len, const uint8_
                    size_t k, size_t t, size_t n, uint8_t* ok, uint8_t* reject_class, uint8_t* out_sig96,
                    uint8_t* group_ok) {
   if (!c) return BLSV_EINVAL;
-  if (!out_sig96 || !ok || !group_ok || t == 0 || (k && !partials))
+  if (!out_sig96 || !ok || !group_ok || t == 0 || (k && !partials) || (msg_len && !msg))
     return fail(c, BLSV_EINVAL, "aggregate: bad arguments");
   (void)hipSetDevice(c->device);
   std::vector<uint8_t> cls;
