@@ -11,6 +11,20 @@ namespace blsk {
 
 // line slot of (step, pair): 6 Fp slots (a0, a1, a4 as Fp2)
 DI int line_slot(int step, int k) { return (step * 2 + k) * 6; }
+// cache policy of the line staging's stores and loads (soa.h AUX; 0 = default)
+// Cache policy of the line staging: written once by k_miller_lines, read once by k_miller_f, 13.8 KB
+// per beacon -- nothing to keep in L2/MALL. Non-temporal (gfx950 aux 2) on both sides: Miller
+// 196.2 -> 192.7 ms per 1M on one box, interleaved twice (profiles/r06s_ln_nt_ab.json); the loads
+// carry the gain, the stores alone change nothing.
+#ifndef BLS_LN_AUX
+#define BLS_LN_AUX 2
+#endif
+#ifndef BLS_LN_AUX_ST
+#define BLS_LN_AUX_ST BLS_LN_AUX
+#endif
+#ifndef BLS_LN_AUX_LD
+#define BLS_LN_AUX_LD BLS_LN_AUX
+#endif
 
 // Item g = base + i of the chunk (H/S/F/cls stride cnt); its lines at LN index i (stride sub).
 // The two pairs run in separate workgroups (k = blockIdx.x & 1: the pair of the whole wave), so a
@@ -59,9 +73,9 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
     auto emit = [&](int step, const line& l) {
       const int s = line_slot(step, k);
       const line o = act[k] ? l : line_one();
-      st_fp2(LN, sub, i, s + 0, o.a0);
-      st_fp2(LN, sub, i, s + 2, o.a1);
-      st_fp2(LN, sub, i, s + 4, o.a4);
+      st_fp2<BLS_LN_AUX_ST>(LN, sub, i, s + 0, o.a0);
+      st_fp2<BLS_LN_AUX_ST>(LN, sub, i, s + 2, o.a1);
+      st_fp2<BLS_LN_AUX_ST>(LN, sub, i, s + 4, o.a4);
     };
     // call-free steps (pairing.h miller_dbl_step_inl): P, Q and the lines never live across a call
     auto pcoord = [&](int c) {
@@ -78,7 +92,7 @@ k_miller_lines(const uint32_t* pk_tab, const uint8_t* pk_inf, const uint32_t* pk
       return;
     }
     int step = 0;
-    auto put = [&](int c, const fp2& v) { st_fp2(LN, sub, i, line_slot(step, k) + 2 * c, v); };
+    auto put = [&](int c, const fp2& v) { st_fp2<BLS_LN_AUX_ST>(LN, sub, i, line_slot(step, k) + 2 * c, v); };
     auto xp = [&]() { return pcoord(0); };
     auto yp = [&]() { return pcoord(1); };
     // T parks in LDS (72 words per lane, word-major: 18 KB per one-wave workgroup, 8 per CU at 2
@@ -161,7 +175,8 @@ BLS_KERNEL(BLS_WPE_MILLER_F) k_miller_f(const uint32_t* LN, const uint8_t* cls, 
   if (cls[g] != REJ_OK) return;
   auto load = [&](int step, int k) {
     const int s = line_slot(step, k);
-    return line{ld_fp2(LN, sub, i, s + 0), ld_fp2(LN, sub, i, s + 2), ld_fp2(LN, sub, i, s + 4)};
+    return line{ld_fp2<BLS_LN_AUX_LD>(LN, sub, i, s + 0), ld_fp2<BLS_LN_AUX_LD>(LN, sub, i, s + 2),
+                ld_fp2<BLS_LN_AUX_LD>(LN, sub, i, s + 4)};
   };
   // miller_f_from_lines (pairing.h) with the line-pair product parked in LDS
   fp12 f = fp12_one();

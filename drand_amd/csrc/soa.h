@@ -8,11 +8,13 @@ namespace bls {
 
 
 #ifdef BLS_HOST
+template <int AUX = 0>
 DI void st_fp(uint32_t* buf, size_t n, size_t i, int slot, const fp& a) {
 #pragma unroll
   for (int k = 0; k < 12; k++) buf[(size_t)(slot * 12 + k) * n + i] = a.l[k];
 }
 
+template <int AUX = 0>
 DI fp ld_fp(const uint32_t* buf, size_t n, size_t i, int slot) {
   fp a;
 #pragma unroll
@@ -37,17 +39,20 @@ DI uint32_t soa_word_off(size_t n, int k) {
   asm volatile("" : "+s"(n4));
   return (uint32_t)k * n4;
 }
+// AUX: the cache-policy bits of the access (0: default; gfx950 NT = 2 streams past the caches)
+template <int AUX = 0>
 DI void st_fp(uint32_t* buf, size_t n, size_t i, int slot, const fp& a) {
   const __amdgpu_buffer_rsrc_t r = soa_slot_rsrc(buf, n, slot);
 #pragma unroll
-  for (int k = 0; k < 12; k++) __builtin_amdgcn_raw_buffer_store_b32(a.l[k], r, (uint32_t)(i * 4), soa_word_off(n, k), 0);
+  for (int k = 0; k < 12; k++) __builtin_amdgcn_raw_buffer_store_b32(a.l[k], r, (uint32_t)(i * 4), soa_word_off(n, k), AUX);
 }
 
+template <int AUX = 0>
 DI fp ld_fp(const uint32_t* buf, size_t n, size_t i, int slot) {
   const __amdgpu_buffer_rsrc_t r = soa_slot_rsrc(buf, n, slot);
   fp a;
 #pragma unroll
-  for (int k = 0; k < 12; k++) a.l[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(i * 4), soa_word_off(n, k), 0);
+  for (int k = 0; k < 12; k++) a.l[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(i * 4), soa_word_off(n, k), AUX);
   return a;
 }
 #endif
@@ -88,13 +93,15 @@ DI fp2 ld_fp2_v(const uint32_t* buf, size_t n, size_t i, int slot) {
   return {ld_fp_v(buf, n, i, slot), ld_fp_v(buf, n, i, slot + 1)};
 }
 
+template <int AUX = 0>
 DI void st_fp2(uint32_t* buf, size_t n, size_t i, int slot, const fp2& a) {
-  st_fp(buf, n, i, slot, a.c0);
-  st_fp(buf, n, i, slot + 1, a.c1);
+  st_fp<AUX>(buf, n, i, slot, a.c0);
+  st_fp<AUX>(buf, n, i, slot + 1, a.c1);
 }
 
+template <int AUX = 0>
 DI fp2 ld_fp2(const uint32_t* buf, size_t n, size_t i, int slot) {
-  return {ld_fp(buf, n, i, slot), ld_fp(buf, n, i, slot + 1)};
+  return {ld_fp<AUX>(buf, n, i, slot), ld_fp<AUX>(buf, n, i, slot + 1)};
 }
 
 DI void st_fp12(uint32_t* buf, size_t n, size_t i, const fp12& a) {

@@ -22,6 +22,7 @@
 #   variant:NAME     GPU suite + bench on variants/libblsverify_NAME.so (scripts/build_variant.sh,
 #                    loaded through DRAND_AMD_LIB)
 #   vbench:NAME      bench only on that variant (same-box A/B against a plain `bench` step)
+#   ab:N1,N2,..      base and each variant interleaved, two passes (bench_<name>_<pass>.json)
 #   vlat:NAME        tools/latency_bench.py on that variant (same-box A/B against a plain `lat` step)
 set -o pipefail
 export TMPDIR=/tmp
@@ -97,6 +98,18 @@ for step in "$@"; do
         DRAND_AMD_LIB=$L timeout -k 10 300 python -u tools/latency_bench.py --reps 10 --out "$O/latency_$V.json" \
           > "$O/latency_$V.log" 2>&1 || rc=32
       fi ;;
+    ab:*)
+      # interleaved same-box A/B: base and each variant, two passes (bench_<name>_<pass>.json)
+      IFS=, read -ra VS <<< "${step#ab:}"
+      for pass in 1 2; do
+        timeout -k 10 400 python -u bench.py --cpu-per-worker 0 > "$O/bench_base_$pass.json" 2> "$O/bench_base_$pass.err" || { rc=33; break; }
+        for V in "${VS[@]}"; do
+          L=variants/libblsverify_$V.so
+          [ -f "$L" ] || { echo "no $L"; rc=30; break 2; }
+          DRAND_AMD_LIB=$L timeout -k 10 400 python -u bench.py --cpu-per-worker 0 > "$O/bench_${V}_$pass.json" \
+            2> "$O/bench_${V}_$pass.err" || { rc=33; break 2; }
+        done
+      done ;;
     vbench:*)
       V=${step#vbench:}
       L=variants/libblsverify_$V.so
