@@ -38,12 +38,18 @@ def is_tri(name):
     return "_tri" in name.split("(")[0]
 
 
-def totals(path, counter, tri_factor=None):
+def kernel_of(name):
+    return name.split("(")[0].replace("void ", "").replace("blsk::", "")
+
+
+def totals(path, counter, tri_factor=None, per_kernel=False):
     out = defaultdict(float)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
         st = stage_of(r["Kernel_Name"])
+        if st and per_kernel:
+            st = kernel_of(r["Kernel_Name"])
         if st:
             v = float(r["Counter_Value"]) * 1024.0
             if tri_factor is not None:
@@ -68,6 +74,13 @@ def main():
     for st in sorted(set(cf) | set(cw)):
         rd, wr = cf.get(st, 0.0) / n, cw.get(st, 0.0) / n
         res["calibrated_bytes_per_beacon"][st] = {"read": round(rd, 1), "write": round(wr, 1), "total": round(rd + wr, 1)}
+    # per kernel, guide's x2 (the Miller targets are per kernel: k_miller_f reads / writes)
+    kf = totals(sys.argv[1], "FETCH_SIZE", per_kernel=True)
+    kw = totals(sys.argv[2], "WRITE_SIZE", per_kernel=True)
+    res["kernel_bytes_per_beacon"] = {}
+    for k in sorted(set(kf) | set(kw)):
+        rd, wr = 2 * kf.get(k, 0.0) / n, kw.get(k, 0.0) / n
+        res["kernel_bytes_per_beacon"][k] = {"read": round(rd, 1), "write": round(wr, 1)}
     txt = json.dumps(res, indent=1)
     if len(sys.argv) > 4:
         open(sys.argv[4], "w").write(txt + "\n")
