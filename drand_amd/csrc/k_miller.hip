@@ -250,12 +250,12 @@ BLS_KERNEL(BLS_WPE_MILLER_TRI) k_miller_f_tri(const uint32_t* LN, const uint8_t*
     auto la = [&](int c) {
       size_t j = i;
       asm volatile("" : "+v"(j));
-      return ld_fp2_v(LN + (size_t)s0 * 12 * sub, sub, j, 2 * c);
+      return ld_fp2_v<BLS_LN_AUX_LD>(LN + (size_t)s0 * 12 * sub, sub, j, 2 * c);
     };
     auto lb = [&](int c) {
       size_t j = i;
       asm volatile("" : "+v"(j));
-      return ld_fp2_v(LN + (size_t)s1 * 12 * sub, sub, j, 2 * c);
+      return ld_fp2_v<BLS_LN_AUX_LD>(LN + (size_t)s1 * 12 * sub, sub, j, 2 * c);
     };
     const fp4 L = tri_line_pair(t, la, lb);
     if (s == 0) {

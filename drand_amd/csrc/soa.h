@@ -63,6 +63,7 @@ DI fp ld_fp(const uint32_t* buf, size_t n, size_t i, int slot) {
 // host form is the same as st_fp / ld_fp.
 #ifdef BLS_HOST
 DI void st_fp_v(uint32_t* buf, size_t n, size_t i, int slot, const fp& a) { st_fp(buf, n, i, slot, a); }
+template <int AUX = 0>
 DI fp ld_fp_v(const uint32_t* buf, size_t n, size_t i, int slot) { return ld_fp(buf, n, i, slot); }
 #else
 DI __amdgpu_buffer_rsrc_t soa_obj_rsrc(const uint32_t* buf, size_t n, int slots) {
@@ -76,12 +77,13 @@ DI void st_fp_v(uint32_t* buf, size_t n, size_t i, int slot, const fp& a) {
 #pragma unroll
   for (int k = 0; k < 12; k++) __builtin_amdgcn_raw_buffer_store_b32(a.l[k], r, vo, soa_word_off(n, k), 0);
 }
+template <int AUX = 0>
 DI fp ld_fp_v(const uint32_t* buf, size_t n, size_t i, int slot) {
   const __amdgpu_buffer_rsrc_t r = soa_obj_rsrc(buf, n, 12);
   const uint32_t vo = (uint32_t)(((size_t)slot * 12 * n + i) * 4);
   fp a;
 #pragma unroll
-  for (int k = 0; k < 12; k++) a.l[k] = __builtin_amdgcn_raw_buffer_load_b32(r, vo, soa_word_off(n, k), 0);
+  for (int k = 0; k < 12; k++) a.l[k] = __builtin_amdgcn_raw_buffer_load_b32(r, vo, soa_word_off(n, k), AUX);
   return a;
 }
 #endif
@@ -89,8 +91,9 @@ DI void st_fp2_v(uint32_t* buf, size_t n, size_t i, int slot, const fp2& a) {
   st_fp_v(buf, n, i, slot, a.c0);
   st_fp_v(buf, n, i, slot + 1, a.c1);
 }
+template <int AUX = 0>
 DI fp2 ld_fp2_v(const uint32_t* buf, size_t n, size_t i, int slot) {
-  return {ld_fp_v(buf, n, i, slot), ld_fp_v(buf, n, i, slot + 1)};
+  return {ld_fp_v<AUX>(buf, n, i, slot), ld_fp_v<AUX>(buf, n, i, slot + 1)};
 }
 
 template <int AUX = 0>
