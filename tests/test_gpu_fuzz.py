@@ -9,7 +9,11 @@ pinned to the reference KAT) on inputs no golden file holds.
   a random position (flags, x, the sign bit), the sign bit alone, another message's signature, a
   random 96-byte string with the compression flag set, the infinity encoding with and without stray
   bits: every reject class equals the oracle's, on the latency path and on the batch pipeline.
+
+DRAND_AMD_FUZZ_SCALE=k (default 1) runs k times as many random cases, each block with its own seeds
+(profiles/r06w_pytest_gpu_fuzz_x10.log is one such run).
 """
+import os
 import random
 
 import pytest
@@ -18,6 +22,7 @@ pytestmark = pytest.mark.gpu
 
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 LENGTHS = (0, 1, 31, 32, 33, 63, 64, 65, 100, 135, 136, 137, 200, 255, 256, 300)
+SCALE = max(1, int(os.environ.get("DRAND_AMD_FUZZ_SCALE", "1")))
 
 
 @pytest.fixture(scope="module")
@@ -33,12 +38,13 @@ def _msgs(rng, n):
 
 
 def test_sign_random_messages_equal_oracle(engine, C):
-    rng = random.Random(0x5157)
-    sk = rng.randrange(1, R)
-    msgs = _msgs(rng, 160)
-    got = engine.sign(sk.to_bytes(32, "big"), msgs)
-    bad = [i for i, (m, s) in enumerate(zip(msgs, got)) if s != C.sign(sk, m)]
-    assert not bad, bad[:8]
+    for blk in range(SCALE):
+        rng = random.Random(0x5157 + 1000 * blk)
+        sk = rng.randrange(1, R)
+        msgs = _msgs(rng, 160)
+        got = engine.sign(sk.to_bytes(32, "big"), msgs)
+        bad = [i for i, (m, s) in enumerate(zip(msgs, got)) if s != C.sign(sk, m)]
+        assert not bad, (blk, bad[:8])
 
 
 def _corrupt(rng, sigs, i):
@@ -65,7 +71,11 @@ def _corrupt(rng, sigs, i):
 
 @pytest.mark.parametrize("route", ["lat", "batch"])
 def test_verify_random_corruptions_equal_oracle(engine, golden, C, route):
-    rng = random.Random(0xF022 + (route == "batch"))
+    for blk in range(SCALE):
+        _verify_block(engine, golden, C, route, random.Random(0xF022 + (route == "batch") + 1000 * blk))
+
+
+def _verify_block(engine, golden, C, route, rng):
     ch = golden["chained"]
     sk, pk = int(ch["sk"], 16), bytes.fromhex(ch["pk"])
     msgs = _msgs(rng, 240)
@@ -122,7 +132,7 @@ def test_aggregate_random_rounds_equal_oracle(engine, golden, C):
     rng = random.Random(0xA66)
     h0, m0 = engine.spec_stats()
     rounds = fails = 0
-    for _ in range(14):
+    for _ in range(14 * SCALE):
         parts = [bytes.fromhex(p) for p in th["partials"]]
         rng.shuffle(parts)
         parts = _mangle_shares(rng, parts[:rng.randrange(t - 2, n + 1)], n)
@@ -159,7 +169,7 @@ def test_aggregate_round_v1_v2_random_equal_oracle(engine, golden, C):
     grp = C.Group(commits)
     rng = random.Random(0xB22)
     seen = set()
-    for _ in range(12):
+    for _ in range(12 * SCALE):
         p1 = [bytes.fromhex(p) for p in th["partials"]]
         p2 = [bytes.fromhex(p) for p in th["partials_v2"]]
         rng.shuffle(p1)
