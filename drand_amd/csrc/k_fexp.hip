@@ -48,6 +48,9 @@ template <int MODE>
 BLS_KERNEL(BLS_WPE_FEXP_TRI) k_fexp_tri(const uint32_t* X, const uint32_t* C, const uint32_t* G, size_t cnt,
                                         uint8_t* cls, uint32_t* OUT, uint32_t* park) {
   const tri_lane t = tri_lane_id();
+#if BLS_CSQR_LIN
+  tri_kp_init();
+#endif
   const size_t ir = (size_t)blockIdx.x * TRI_GROUPS + t.group;
   const bool in_range = t.group < TRI_GROUPS && ir < cnt;
   const size_t i0 = in_range ? ir : cnt - 1;  // dummy lanes compute on a real row, never store

@@ -97,6 +97,98 @@ DI fp2 fp2_addsub(const fp2& a, const fp2& b, bool sub) {  // fp.h fp_addsub on 
   }
   return r;
 }
+// 3u + 2x (sub = false) or 3u - 2x (sub = true) per component, for u, x in [0, 2p), the result in
+// [0, 2p): the Granger-Scott post-square combination (tri.h tri_cyclotomic_sqr) as one linear form and
+// ONE reduction by an estimated multiple of p, instead of fp2_addsub + fp2_dbl + fp2_add (three):
+//   y = sub ? 2p - x : x              in [0, 2p]
+//   t = 2(u + y) + u                  in [0, 10p): 385 bits, hi = the carry out of word 11
+//   q = floor(T / D), T = t >> 352 (33 bits), D = P11 + 1 (p's top word + 1): a float estimate that
+//       is q or q - 1, then one exact 64-bit comparison
+//   r = t - q p                       (q p from KP: a MAD chain, or tri.h's LDS table of k p)
+// r >= 0: q p <= T p / D < T 2^352 <= t (p < D 2^352). r < 2p: q > T/D - 1 and p >= P11 2^352 give
+// t - q p < 2^352 (T/D + 1) + p <= 11 * 2^352 + p (T/D < 10), and 11 * 2^352 < p / 10^7.
+DI uint32_t fp_quot_top(const uint32_t (&t)[12], uint32_t hi) {
+  constexpr uint32_t D = P_RAW[11] + 1u;
+  // float(T) is within 2^10 of T and the product within 2^-22 relative: the estimate is within
+  // 4e-6 of T / D, so subtracting 1e-4 makes it floor(T / D) or one less (clamped at 0)
+  float e = ((float)t[11] + (float)hi * 4294967296.0f) * (1.0f / (float)D) - 1e-4f;
+  e = e > 0.0f ? e : 0.0f;
+  uint32_t q = (uint32_t)e;
+  const uint64_t T = ((uint64_t)hi << 32) | t[11];
+  return q + (T >= (uint64_t)(q + 1u) * D ? 1u : 0u);
+}
+// q p as 12 words (q <= 10: < 11p < 2^385, the 13th word is not needed: t - q p < 2^384) by a MAD
+// chain; tri.h reads it from an LDS table instead
+struct KpMad {
+  DI u12 operator()(uint32_t q) const {
+    u12 w;
+    uint64_t k = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      k = (uint64_t)q * P_RAW[i] + (k >> 32);
+      w[i] = (uint32_t)k;
+    }
+    return w;
+  }
+};
+// N components at once (the cyclotomic square passes all four of its outputs): every carry chain is
+// written interleaved across the N components, so no chain link waits for its predecessor (fp.h)
+template <int N, typename KP = KpMad>
+DI void fp_3u_pm_2x_n(const fp (&u)[N], const fp (&x)[N], const bool (&sub)[N], fp (&r)[N], KP kp = KP()) {
+  uint32_t y[N][12];
+  {
+    uint32_t d[N][12];
+    unsigned b[N];
+#pragma unroll
+    for (int c = 0; c < N; c++) b[c] = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++)
+#pragma unroll
+      for (int c = 0; c < N; c++) d[c][i] = __builtin_subc(P2_RAW[i], x[c].l[i], b[c], &b[c]);
+#pragma unroll
+    for (int i = 0; i < 12; i++)
+#pragma unroll
+      for (int c = 0; c < N; c++) y[c][i] = sub[c] ? d[c][i] : x[c].l[i];
+  }
+  uint32_t t[N][12];
+  unsigned h[N];
+  {
+    uint32_t w[N][12];
+    unsigned cs[N], cw[N];
+#pragma unroll
+    for (int c = 0; c < N; c++) cs[c] = cw[c] = h[c] = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++)
+#pragma unroll
+      for (int c = 0; c < N; c++) {  // s = u + y < 4p, 2s < 8p < 2^384: no carry out of either
+        const uint32_t si = __builtin_addc(u[c].l[i], y[c][i], cs[c], &cs[c]);
+        w[c][i] = __builtin_addc(si, si, cw[c], &cw[c]);
+      }
+#pragma unroll
+    for (int i = 0; i < 12; i++)
+#pragma unroll
+      for (int c = 0; c < N; c++) t[c][i] = __builtin_addc(w[c][i], u[c].l[i], h[c], &h[c]);
+  }
+  u12 qp[N];
+#pragma unroll
+  for (int c = 0; c < N; c++) qp[c] = kp(fp_quot_top(t[c], h[c]));
+  unsigned b[N];
+#pragma unroll
+  for (int c = 0; c < N; c++) b[c] = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++)
+#pragma unroll
+    for (int c = 0; c < N; c++) r[c].l[i] = __builtin_subc(t[c][i], qp[c][i], b[c], &b[c]);
+}
+template <typename KP = KpMad>
+DI fp2 fp2_3u_pm_2x(const fp2& u, const fp2& x, bool sub, KP kp = KP()) {
+  const fp uu[2] = {u.c0, u.c1}, xx[2] = {x.c0, x.c1};
+  const bool ss[2] = {sub, sub};
+  fp r[2];
+  fp_3u_pm_2x_n<2>(uu, xx, ss, r, kp);
+  return {r[0], r[1]};
+}
+
 DI fp2 fp2_neg(const fp2& a) {  // fp_neg per component, the two chains interleaved
   uint32_t d0[12], d1[12];
   unsigned b0 = 0, b1 = 0;

@@ -280,6 +280,9 @@ DI fp4 tri_conj(const tri_lane& t, const fp4& x) {
 #ifndef BLS_CSQR_PARK
 #define BLS_CSQR_PARK 1
 #endif
+#ifndef BLS_CSQR_LIN
+#define BLS_CSQR_LIN 1
+#endif
 // x parked in this lane's first 48 words of g_tri_arg (the staging slots 0 and 1, free between the
 // products) as 12 16-byte columns: the square's limb arrays then have the register file to themselves
 // (with x held across the square, the K7 body spilled 24 dwords per square to scratch: 18 KB of HBM
@@ -310,6 +313,36 @@ DI fp4 tri_unpark4() {
   return x;
 }
 
+// k p for k = 0..10 (12 words each, 16-byte aligned rows of 3 uint4): the reduction multiple of the
+// fused 3u +- 2x (tower.h fp2_3u_pm_2x) read per lane from LDS (3 ds_read_b128) instead of a 12-MAD
+// chain. Written once per workgroup by tri_kp_init (k_fexp_tri), 528 bytes.
+static __shared__ __attribute__((aligned(16))) uint32_t g_kp_tab[11 * 12];
+DI void tri_kp_init() {
+  for (unsigned j = threadIdx.x; j < 11u * 12u; j += blockDim.x) {
+    const uint32_t k = j / 12u, word = j % 12u;
+    uint64_t c = 0;
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      c = (uint64_t)k * P_RAW[i] + (c >> 32);
+      if ((uint32_t)i == word) w = (uint32_t)c;
+    }
+    g_kp_tab[j] = w;
+  }
+  __syncthreads();
+}
+struct KpLds {
+  DI u12 operator()(uint32_t q) const {
+    q = q < 10u ? q : 10u;  // q <= 10 by the operand bounds; the clamp keeps the read in the table
+    const uint4* r = reinterpret_cast<const uint4*>(g_kp_tab) + 3u * q;
+    const uint4 a = r[0], b = r[1], c = r[2];
+    u12 w;
+    w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y;
+    w[6] = b.z, w[7] = b.w, w[8] = c.x, w[9] = c.y, w[10] = c.z, w[11] = c.w;
+    return w;
+  }
+};
+
 DI fp4 tri_cyclotomic_sqr(const tri_lane& t, const fp4& x_in) {
 #if BLS_CSQR_PARK
   tri_park4(x_in);
@@ -327,9 +360,18 @@ DI fp4 tri_cyclotomic_sqr(const tri_lane& t, const fp4& x_in) {
   const bool r1 = t.role == 1;
   const fp2 u = fp2_select(r1, fp2_mul_xi(y.b), y.a);
   const fp2 v = fp2_select(r1, y.a, y.b);
+#if BLS_CSQR_LIN
+  // 3u +- 2a as one linear form and one reduction (tower.h fp2_3u_pm_2x), direction by role
+  const fp uu[4] = {u.c0, u.c1, v.c0, v.c1}, xx[4] = {x.a.c0, x.a.c1, x.b.c0, x.b.c1};
+  const bool ss[4] = {!r1, !r1, r1, r1};
+  fp o[4];
+  fp_3u_pm_2x_n<4>(uu, xx, ss, o, KpLds());
+  return {{o[0], o[1]}, {o[2], o[3]}};
+#else
   // 3u +- 2a = 2(u +- a) + u: one direction-by-role addition instead of both and a select
   const fp2 ta = fp2_addsub(u, x.a, !r1), tb = fp2_addsub(v, x.b, r1);
   return {fp2_add(fp2_dbl(ta), u), fp2_add(fp2_dbl(tb), v)};
+#endif
 }
 
 // general product (Karatsuba over the cubic): lane j forms P_j = A_j B_j and

@@ -160,6 +160,16 @@ def test_host_cofactor_addition_flags_exceptions(opcount_bin):
     assert json.loads(r.stdout)["add_mismatch"] == 0
 
 
+def test_fused_cyclotomic_combination_host(opcount_bin):
+    """tower.h fp2_3u_pm_2x, the 3-lane cyclotomic square's 3u +- 2x with one reduction by an estimated
+    multiple of p, equals fp2_addsub + fp2_dbl + fp2_add mod p and stays in [0, 2p) on random
+    operands, the range edges and operands aimed at every boundary of its quotient correction."""
+    r = subprocess.run([opcount_bin, "linfuzz", "3000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout)
+    assert out["lin_mismatch"] == 0 and out["boundary_cases"] > 10000
+
+
 def _split_top(args):
     out, depth, cur = [], 0, ""
     for ch in args:

@@ -300,11 +300,75 @@ static int cmd_addfuzz(unsigned long n) {
   return bad != 0;
 }
 
+// tower.h fp2_3u_pm_2x (the cyclotomic square's fused 3u +- 2x) against fp2_addsub + fp2_dbl +
+// fp2_add on random operands in [0, 2p), the edges 0 and 2p - 1, and top words placed so that the
+// quotient estimate sits on each boundary k D (k = 1..10) of its correction step; every result must
+// equal the reference mod p and lie in [0, 2p).
+static int cmd_linfuzz(unsigned long n) {
+  using namespace bls;
+  unsigned long long s = 0x9e3779b97f4a7c15ull;
+  auto next = [&]() {
+    s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+    return (uint32_t)(s >> 11);
+  };
+  auto below2p = [&](uint32_t top) {  // top word < P2_RAW[11]: the value is < 2p
+    fp x;
+    for (int i = 0; i < 11; i++) x.l[i] = next();
+    x.l[11] = top;
+    return x;
+  };
+  auto rnd = [&]() { return below2p(next() % P2_RAW[11]); };
+  fp zero = fp_zero(), max2p;
+  {
+    unsigned br = 0;
+    for (int i = 0; i < 12; i++) max2p.l[i] = __builtin_subc(P2_RAW[i], i == 0 ? 1u : 0u, br, &br);
+  }
+  auto lt2p = [](const fp& a) {
+    unsigned br = 0;
+    for (int i = 0; i < 12; i++) (void)__builtin_subc(a.l[i], P2_RAW[i], br, &br);
+    return br != 0;
+  };
+  unsigned long bad = 0, cases = 0, edges = 0;
+  auto check = [&](const fp2& u, const fp2& x, bool sub) {
+    const fp2 got = fp2_3u_pm_2x(u, x, sub);
+    const fp2 want = fp2_add(fp2_dbl(fp2_addsub(u, x, sub)), u);
+    bad += !(fp_eq(got.c0, want.c0) && fp_eq(got.c1, want.c1) && lt2p(got.c0) && lt2p(got.c1));
+    cases++;
+  };
+  const uint32_t D = P_RAW[11] + 1u;
+  for (unsigned long t = 0; t < n; t++) {
+    for (int sub = 0; sub < 2; sub++) {
+      check({rnd(), rnd()}, {rnd(), rnd()}, sub);
+      check({zero, max2p}, {max2p, zero}, sub);
+      check({max2p, max2p}, {max2p, max2p}, sub);
+      check({zero, zero}, {zero, zero}, sub);
+    }
+    // T = t >> 352 ~ 3 u11 + 2 y11 (+ carries), y = x or 2p - x: aim it at k D - 1, k D, k D + 1
+    for (uint32_t k = 1; k <= 10; k++) {
+      for (int d = -1; d <= 1; d++) {
+        const int64_t T = (int64_t)k * D + d;
+        const uint32_t a = next() % P2_RAW[11];  // u's top word
+        const int64_t b = (T - 3 * (int64_t)a) / 2;  // y's top word
+        if (b < 0 || b >= (int64_t)P2_RAW[11]) continue;
+        // sub = false: y = x
+        check({below2p(a), rnd()}, {below2p((uint32_t)b), rnd()}, false);
+        // sub = true: y = 2p - x, so x's top word ~ P2_11 - b
+        const int64_t bx = (int64_t)P2_RAW[11] - 1 - b;
+        if (bx >= 0) check({below2p(a), rnd()}, {below2p((uint32_t)bx), rnd()}, true);
+        edges++;
+      }
+    }
+  }
+  printf("{\"cases\": %lu, \"boundary_cases\": %lu, \"lin_mismatch\": %lu}\n", cases, edges, bad);
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
   if (argc == 3 && !strcmp(argv[1], "hash")) return cmd_hash(argv[2]);
   if (argc == 3 && !strcmp(argv[1], "powfuzz")) return cmd_powfuzz(strtoul(argv[2], nullptr, 10));
   if (argc == 3 && !strcmp(argv[1], "invfuzz")) return cmd_invfuzz(strtoul(argv[2], nullptr, 10));
   if (argc == 3 && !strcmp(argv[1], "addfuzz")) return cmd_addfuzz(strtoul(argv[2], nullptr, 10));
+  if (argc == 3 && !strcmp(argv[1], "linfuzz")) return cmd_linfuzz(strtoul(argv[2], nullptr, 10));
   if (argc != 5) {
     fprintf(stderr, "usage: %s pk48hex round prevhex|- sig96hex   (prev '-' = unchained V2)\n       %s hash msghex\n",
             argv[0], argv[0]);
