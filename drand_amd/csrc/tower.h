@@ -339,7 +339,150 @@ DI bool fp6_eq(const fp6& a, const fp6& b) { return fp2_eq(a.c0, b.c0) & fp2_eq(
 // multiply by v: (a0 + a1 v + a2 v^2) v = xi a2 + a0 v + a1 v^2
 DI fp6 fp6_mul_v(const fp6& a) { return {fp2_mul_xi(a.c2), a.c0, a.c1}; }
 
-DI fp6 fp6_mul(const fp6& a, const fp6& b) {  // Karatsuba, 6 Fp2 mul
+// ---- linear forms with one reduction (BLS_F6_LIN): an output that is a signed sum of Fp values
+// in [0, 2p) is formed as T = P + (k p - N) from two lazily added sums P, N < 2^384 (N < k p) and
+// reduced ONCE by q p, q = floor(T / 2^352 / (P11 + 1)) (fp_quot_top, T < 16p so q <= 15), instead
+// of one conditional correction per addition, subtraction and multiplication by xi. KP supplies q p.
+#ifndef BLS_F6_LIN
+#define BLS_F6_LIN 1
+#endif
+struct Words12 {
+  uint32_t w[12];
+};
+constexpr Words12 kp_words(uint32_t k) {
+  Words12 r{};
+  uint64_t c = 0;
+  for (int i = 0; i < 12; i++) {
+    c = (uint64_t)k * P_RAW[i] + (c >> 32);
+    r.w[i] = (uint32_t)c;
+  }
+  return r;
+}
+// the last step of every linear form: r_j = T_j - q_j p for the 385-bit T_j (hi_j = bit 384)
+template <typename KP>
+DI fp2 fp2_lin_reduce(const uint32_t (&t0)[12], unsigned h0, const uint32_t (&t1)[12], unsigned h1, KP kp) {
+  const u12 w0 = kp(fp_quot_top(t0, h0)), w1 = kp(fp_quot_top(t1, h1));
+  fp2 r;
+  unsigned b0 = 0, b1 = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    r.c0.l[i] = __builtin_subc(t0[i], w0[i], b0, &b0);
+    r.c1.l[i] = __builtin_subc(t1[i], w1[i], b1, &b1);
+  }
+  return r;
+}
+// The Karatsuba Fp6 outputs from its six Fp2 products (t_j = a_j b_j, m_jk = (a_j + a_k)(b_j + b_k),
+// every component in [0, 2p)):
+//   c0 = xi (m12 - t1 - t2) + t0,  c1 = m01 - t0 - t1 + xi t2,  c2 = m02 - t0 - t2 + t1
+// with xi (x + y i) = (x - y) + (x + y) i written out per component (u = t1 + t2):
+//   c0 = (m12_0 + u_1 + t0_0 + 6p - (m12_1 + u_0),      m12_0 + m12_1 + t0_1 + 8p - (u_0 + u_1))
+//   c1 = (m01_0 + t2_0 + 6p - (t0_0 + t1_0 + t2_1),      m01_1 + t2_0 + t2_1 + 4p - (t0_1 + t1_1))
+//   c2 = (m02_0 + t1_0 + 4p - (t0_0 + t2_0),             m02_1 + t1_1 + 4p - (t0_1 + t2_1))
+// Every partial sum stays below 8p < 2^384 and every T below 14p (q <= 13). The sums run as four to
+// six carry chains interleaved word by word: a carry link then never waits for the previous one
+// (two interleaved chains still cost an s_nop per link on gfx950).
+template <typename KP>
+DI fp2 kara6_c0(const fp2& m12, const fp2& t0, const fp2& t1, const fp2& t2, KP kp) {
+  constexpr Words12 B0 = kp_words(6), B1 = kp_words(8);
+  uint32_t pa0[12], pa1[12], na0[12], na1[12];
+  {
+    unsigned cu0 = 0, cu1 = 0, c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      const uint32_t u0 = __builtin_addc(t1.c0.l[i], t2.c0.l[i], cu0, &cu0);
+      const uint32_t u1 = __builtin_addc(t1.c1.l[i], t2.c1.l[i], cu1, &cu1);
+      pa0[i] = __builtin_addc(m12.c0.l[i], u1, c0, &c0);
+      pa1[i] = __builtin_addc(m12.c0.l[i], m12.c1.l[i], c1, &c1);
+      na0[i] = __builtin_addc(m12.c1.l[i], u0, c2, &c2);
+      na1[i] = __builtin_addc(u0, u1, c3, &c3);
+    }
+  }
+  uint32_t T0[12], T1[12];
+  unsigned h0 = 0, h1 = 0;
+  {
+    unsigned c0 = 0, c1 = 0, b0 = 0, b1 = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      const uint32_t p0 = __builtin_addc(pa0[i], t0.c0.l[i], c0, &c0);
+      const uint32_t p1 = __builtin_addc(pa1[i], t0.c1.l[i], c1, &c1);
+      const uint32_t n0 = __builtin_subc(B0.w[i], na0[i], b0, &b0);
+      const uint32_t n1 = __builtin_subc(B1.w[i], na1[i], b1, &b1);
+      T0[i] = __builtin_addc(p0, n0, h0, &h0);
+      T1[i] = __builtin_addc(p1, n1, h1, &h1);
+    }
+  }
+  return fp2_lin_reduce(T0, h0, T1, h1, kp);
+}
+template <typename KP>
+DI fp2 kara6_c1(const fp2& m01, const fp2& t0, const fp2& t1, const fp2& t2, KP kp) {
+  constexpr Words12 B0 = kp_words(6), B1 = kp_words(4);
+  uint32_t pa0[12], pa1[12], na0[12], na1[12];
+  {
+    unsigned c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      pa0[i] = __builtin_addc(m01.c0.l[i], t2.c0.l[i], c0, &c0);
+      pa1[i] = __builtin_addc(m01.c1.l[i], t2.c0.l[i], c1, &c1);
+      na0[i] = __builtin_addc(t0.c0.l[i], t1.c0.l[i], c2, &c2);
+      na1[i] = __builtin_addc(t0.c1.l[i], t1.c1.l[i], c3, &c3);
+    }
+  }
+  uint32_t T0[12], T1[12];
+  unsigned h0 = 0, h1 = 0;
+  {
+    unsigned c1 = 0, c2 = 0, b0 = 0, b1 = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      const uint32_t p1 = __builtin_addc(pa1[i], t2.c1.l[i], c1, &c1);
+      const uint32_t m0 = __builtin_addc(na0[i], t2.c1.l[i], c2, &c2);
+      const uint32_t n0 = __builtin_subc(B0.w[i], m0, b0, &b0);
+      const uint32_t n1 = __builtin_subc(B1.w[i], na1[i], b1, &b1);
+      T0[i] = __builtin_addc(pa0[i], n0, h0, &h0);
+      T1[i] = __builtin_addc(p1, n1, h1, &h1);
+    }
+  }
+  return fp2_lin_reduce(T0, h0, T1, h1, kp);
+}
+template <typename KP>
+DI fp2 kara6_c2(const fp2& m02, const fp2& t0, const fp2& t1, const fp2& t2, KP kp) {
+  constexpr Words12 B = kp_words(4);
+  uint32_t T0[12], T1[12];
+  unsigned h0 = 0, h1 = 0;
+  {
+    unsigned c0 = 0, c1 = 0, c2 = 0, c3 = 0, b0 = 0, b1 = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      const uint32_t p0 = __builtin_addc(m02.c0.l[i], t1.c0.l[i], c0, &c0);
+      const uint32_t p1 = __builtin_addc(m02.c1.l[i], t1.c1.l[i], c1, &c1);
+      const uint32_t s0 = __builtin_addc(t0.c0.l[i], t2.c0.l[i], c2, &c2);
+      const uint32_t s1 = __builtin_addc(t0.c1.l[i], t2.c1.l[i], c3, &c3);
+      const uint32_t n0 = __builtin_subc(B.w[i], s0, b0, &b0);
+      const uint32_t n1 = __builtin_subc(B.w[i], s1, b1, &b1);
+      T0[i] = __builtin_addc(p0, n0, h0, &h0);
+      T1[i] = __builtin_addc(p1, n1, h1, &h1);
+    }
+  }
+  return fp2_lin_reduce(T0, h0, T1, h1, kp);
+}
+
+// fp6_mul with one reduction per output component; b's components through lb(c) (k_miller.hip reads
+// them from LDS)
+template <typename LB, typename KP>
+DI fp6 fp6_mul_lin_lb(const fp6& a, LB lb, KP kp) {
+  const fp2 t0 = fp2_mul(a.c0, lb(0));
+  const fp2 t1 = fp2_mul(a.c1, lb(1));
+  const fp2 t2 = fp2_mul(a.c2, lb(2));
+  const fp2 c0 = kara6_c0(fp2_mul(fp2_add_lazy(a.c1, a.c2), fp2_add_lazy(lb(1), lb(2))), t0, t1, t2, kp);
+  const fp2 c1 = kara6_c1(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(lb(0), lb(1))), t0, t1, t2, kp);
+  const fp2 c2 = kara6_c2(fp2_mul(fp2_add_lazy(a.c0, a.c2), fp2_add_lazy(lb(0), lb(2))), t0, t1, t2, kp);
+  return {c0, c1, c2};
+}
+template <typename KP = KpMad>
+DI fp6 fp6_mul_lin(const fp6& a, const fp6& b, KP kp = KP()) {
+  return fp6_mul_lin_lb(a, [&](int c) { return c == 0 ? b.c0 : (c == 1 ? b.c1 : b.c2); }, kp);
+}
+
+DI fp6 fp6_mul(const fp6& a, const fp6& b) {  // Karatsuba, 6 Fp2 mul, a reduction per operation
   fp2 t0 = fp2_mul(a.c0, b.c0);
   fp2 t1 = fp2_mul(a.c1, b.c1);
   fp2 t2 = fp2_mul(a.c2, b.c2);
@@ -403,6 +546,16 @@ DI fp12 fp12_mul(const fp12& a, const fp12& b) {  // Karatsuba, 3 Fp6 mul
   fp6 t1 = fp6_mul(a.c1, b.c1);
   fp6 c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add_lazy(a.c0, a.c1), fp6_add_lazy(b.c0, b.c1)), t0), t1);
   fp6 c0 = fp6_add(t0, fp6_mul_v(t1));
+  return {c0, c1};
+}
+
+// fp12_sqr with the one-reduction Fp6 products (k_miller.hip's f pass, q p from its LDS table)
+template <typename KP>
+DI fp12 fp12_sqr_lin(const fp12& a, KP kp) {
+  fp6 ab = fp6_mul_lin(a.c0, a.c1, kp);
+  fp6 t = fp6_mul_lin(fp6_add_lazy(a.c0, a.c1), fp6_add_lazy(a.c0, fp6_mul_v(a.c1)), kp);
+  fp6 c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab));
+  fp6 c1 = fp6_add(ab, ab);
   return {c0, c1};
 }
 

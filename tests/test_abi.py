@@ -170,6 +170,15 @@ def test_fused_cyclotomic_combination_host(opcount_bin):
     assert out["lin_mismatch"] == 0 and out["boundary_cases"] > 10000
 
 
+def test_one_reduction_fp6_product_host(opcount_bin):
+    """tower.h fp6_mul_lin / fp12_sqr_lin (the Karatsuba Fp6 outputs as linear forms reduced once, the
+    Miller f pass's products) equal fp6_mul / fp12_sqr mod p and stay in [0, 2p): random operands,
+    operands at 2p - 1 and the lazily added (< 4p) operands of the squaring's second product."""
+    r = subprocess.run([opcount_bin, "f6fuzz", "2000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert json.loads(r.stdout)["f6_mismatch"] == 0
+
+
 def _split_top(args):
     out, depth, cur = [], 0, ""
     for ch in args:

@@ -363,12 +363,69 @@ static int cmd_linfuzz(unsigned long n) {
   return bad ? 1 : 0;
 }
 
+// tower.h fp6_mul_lin / fp12_sqr_lin (one reduction per output component, q p by KpMad) against
+// fp6_mul / fp12_sqr: random operands in [0, 2p), operands at 2p - 1, and the lazily added operands
+// (< 4p) fp12_sqr feeds its second product; results equal mod p and in [0, 2p).
+static int cmd_f6fuzz(unsigned long n) {
+  using namespace bls;
+  unsigned long long s = 0x2545f4914f6cdd1dull;
+  auto next = [&]() {
+    s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+    return (uint32_t)(s >> 11);
+  };
+  auto rnd = [&]() {
+    fp x;
+    for (int i = 0; i < 11; i++) x.l[i] = next();
+    x.l[11] = next() % P2_RAW[11];
+    return x;
+  };
+  fp max2p;
+  {
+    unsigned br = 0;
+    for (int i = 0; i < 12; i++) max2p.l[i] = __builtin_subc(P2_RAW[i], i == 0 ? 1u : 0u, br, &br);
+  }
+  auto lt2p = [](const fp& a) {
+    unsigned br = 0;
+    for (int i = 0; i < 12; i++) (void)__builtin_subc(a.l[i], P2_RAW[i], br, &br);
+    return br != 0;
+  };
+  auto r6 = [&](bool edge) {
+    fp6 a;
+    fp2* c[3] = {&a.c0, &a.c1, &a.c2};
+    for (auto* x : c) *x = edge ? fp2{max2p, (next() & 1) ? max2p : rnd()} : fp2{rnd(), rnd()};
+    return a;
+  };
+  auto eq6 = [&](const fp6& x, const fp6& y) {
+    const fp2* a[3] = {&x.c0, &x.c1, &x.c2};
+    const fp2* b[3] = {&y.c0, &y.c1, &y.c2};
+    bool ok = true;
+    for (int k = 0; k < 3; k++)
+      ok &= fp_eq(a[k]->c0, b[k]->c0) && fp_eq(a[k]->c1, b[k]->c1) && lt2p(a[k]->c0) && lt2p(a[k]->c1);
+    return ok;
+  };
+  unsigned long bad = 0, cases = 0;
+  for (unsigned long t = 0; t < n; t++) {
+    for (int e = 0; e < 3; e++) {
+      const fp6 a = r6(e == 1), b = r6(e == 2);
+      bad += !eq6(fp6_mul_lin(a, b), fp6_mul(a, b));
+      const fp6 la = fp6_add_lazy(a, r6(e == 1)), lb = fp6_add_lazy(b, r6(e != 0));  // < 4p
+      bad += !eq6(fp6_mul_lin(la, lb), fp6_mul(la, lb));
+      const fp12 f = {a, b}, g = fp12_sqr_lin(f, KpMad()), h = fp12_sqr(f);
+      bad += !(eq6(g.c0, h.c0) && eq6(g.c1, h.c1));
+      cases += 3;
+    }
+  }
+  printf("{\"cases\": %lu, \"f6_mismatch\": %lu}\n", cases, bad);
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
   if (argc == 3 && !strcmp(argv[1], "hash")) return cmd_hash(argv[2]);
   if (argc == 3 && !strcmp(argv[1], "powfuzz")) return cmd_powfuzz(strtoul(argv[2], nullptr, 10));
   if (argc == 3 && !strcmp(argv[1], "invfuzz")) return cmd_invfuzz(strtoul(argv[2], nullptr, 10));
   if (argc == 3 && !strcmp(argv[1], "addfuzz")) return cmd_addfuzz(strtoul(argv[2], nullptr, 10));
   if (argc == 3 && !strcmp(argv[1], "linfuzz")) return cmd_linfuzz(strtoul(argv[2], nullptr, 10));
+  if (argc == 3 && !strcmp(argv[1], "f6fuzz")) return cmd_f6fuzz(strtoul(argv[2], nullptr, 10));
   if (argc != 5) {
     fprintf(stderr, "usage: %s pk48hex round prevhex|- sig96hex   (prev '-' = unchained V2)\n       %s hash msghex\n",
             argv[0], argv[0]);
