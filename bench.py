@@ -50,7 +50,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 LIMB_PRODUCTS_PER_FP_MUL = 288  # algorithmic unit: 12x32-bit Montgomery = 144 (a*b) + 144 (m*p) limb products
-PMC_FILE = "r06t_pmc_traffic.json"
+PMC_FILE = "r06z_pmc_traffic.json"
 
 
 def load_json(rel):

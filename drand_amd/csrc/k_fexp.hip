@@ -49,7 +49,7 @@ BLS_KERNEL(BLS_WPE_FEXP_TRI) k_fexp_tri(const uint32_t* X, const uint32_t* C, co
                                         uint8_t* cls, uint32_t* OUT, uint32_t* park) {
   const tri_lane t = tri_lane_id();
 #if BLS_CSQR_LIN
-  tri_kp_init();
+  kp_lds_init<11>();
 #endif
   const size_t ir = (size_t)blockIdx.x * TRI_GROUPS + t.group;
   const bool in_range = t.group < TRI_GROUPS && ir < cnt;

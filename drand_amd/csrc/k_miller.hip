@@ -139,34 +139,9 @@ DI fp2 mf_get(int c) {
   }
   return v;
 }
-// k p for k = 0..15 (16-byte aligned rows of 3 uint4): q p of the one-reduction linear forms
-// (tower.h fp2_lin_final, T < 16p) read per lane from LDS; written once per workgroup (768 bytes)
-static __shared__ __attribute__((aligned(16))) uint32_t g_kp16[16 * 12];
-DI void kp16_init() {
-  for (unsigned j = threadIdx.x; j < 16u * 12u; j += blockDim.x) {
-    const uint32_t k = j / 12u, word = j % 12u;
-    uint64_t c = 0;
-    uint32_t w = 0;
-#pragma unroll
-    for (int i = 0; i < 12; i++) {
-      c = (uint64_t)k * P_RAW[i] + (c >> 32);
-      if ((uint32_t)i == word) w = (uint32_t)c;
-    }
-    g_kp16[j] = w;
-  }
-  __syncthreads();
-}
-struct KpLds16 {
-  DI u12 operator()(uint32_t q) const {
-    q = q < 15u ? q : 15u;  // q <= 15 by the operand bounds; the clamp keeps the read in the table
-    const uint4* r = reinterpret_cast<const uint4*>(g_kp16) + 3u * q;
-    const uint4 a = r[0], b = r[1], c = r[2];
-    u12 w;
-    w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y;
-    w[6] = b.z, w[7] = b.w, w[8] = c.x, w[9] = c.y, w[10] = c.z, w[11] = c.w;
-    return w;
-  }
-};
+// q p of the one-reduction linear forms (tower.h fp2_lin_reduce, T < 16p) from an LDS table of k p,
+// k < 16 (768 bytes per workgroup, tower.h kp_lds_init / KpLdsK)
+using KpLds16 = KpLdsK<16>;
 
 // fp6_mul(a, b) (tower.h, Karatsuba) with b's components read through lb
 template <typename LB>
@@ -203,7 +178,7 @@ DI fp12 fp12_mul_by_line_pair_lds(const fp12& f) {
 BLS_KERNEL(BLS_WPE_MILLER_F) k_miller_f(const uint32_t* LN, const uint8_t* cls, size_t cnt, size_t base,
                                                   size_t m, size_t sub, uint32_t* F) {
 #if BLS_F6_LIN
-  kp16_init();  // before the early exits: every lane of the workgroup writes its table words
+  kp_lds_init<16>();  // before the early exits: every lane of the workgroup writes its table words
 #endif
   const size_t i = (size_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= m) return;

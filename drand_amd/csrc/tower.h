@@ -358,6 +358,45 @@ constexpr Words12 kp_words(uint32_t k) {
   }
   return r;
 }
+#ifndef BLS_HOST
+// k p for k < K in LDS, one copy per workgroup (16-byte aligned rows of 3 uint4): the q p of the
+// one-reduction linear forms read per lane (3 ds_read_b128) instead of a 12-MAD chain.
+// kp_lds_init<K>() runs once per workgroup, reached by every lane, before the first use.
+template <int K>
+DI uint32_t* kp_lds_tab() {
+  static __shared__ __attribute__((aligned(16))) uint32_t tab[K * 12];
+  return tab;
+}
+template <int K>
+DI void kp_lds_init() {
+  uint32_t* tab = kp_lds_tab<K>();
+  for (unsigned j = threadIdx.x; j < (unsigned)K * 12u; j += blockDim.x) {
+    const uint32_t k = j / 12u, word = j % 12u;
+    uint64_t c = 0;
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      c = (uint64_t)k * P_RAW[i] + (c >> 32);
+      if ((uint32_t)i == word) w = (uint32_t)c;
+    }
+    tab[j] = w;
+  }
+  __syncthreads();
+}
+template <int K>
+struct KpLdsK {
+  DI u12 operator()(uint32_t q) const {
+    q = q < (uint32_t)(K - 1) ? q : (uint32_t)(K - 1);  // in range by the operand bounds; kept in the table
+    const uint4* r = reinterpret_cast<const uint4*>(kp_lds_tab<K>()) + 3u * q;
+    const uint4 a = r[0], b = r[1], c = r[2];
+    u12 w;
+    w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y;
+    w[6] = b.z, w[7] = b.w, w[8] = c.x, w[9] = c.y, w[10] = c.z, w[11] = c.w;
+    return w;
+  }
+};
+#endif
+
 // the last step of every linear form: r_j = T_j - q_j p for the 385-bit T_j (hi_j = bit 384)
 template <typename KP>
 DI fp2 fp2_lin_reduce(const uint32_t (&t0)[12], unsigned h0, const uint32_t (&t1)[12], unsigned h1, KP kp) {

@@ -313,35 +313,9 @@ DI fp4 tri_unpark4() {
   return x;
 }
 
-// k p for k = 0..10 (12 words each, 16-byte aligned rows of 3 uint4): the reduction multiple of the
-// fused 3u +- 2x (tower.h fp2_3u_pm_2x) read per lane from LDS (3 ds_read_b128) instead of a 12-MAD
-// chain. Written once per workgroup by tri_kp_init (k_fexp_tri), 528 bytes.
-static __shared__ __attribute__((aligned(16))) uint32_t g_kp_tab[11 * 12];
-DI void tri_kp_init() {
-  for (unsigned j = threadIdx.x; j < 11u * 12u; j += blockDim.x) {
-    const uint32_t k = j / 12u, word = j % 12u;
-    uint64_t c = 0;
-    uint32_t w = 0;
-#pragma unroll
-    for (int i = 0; i < 12; i++) {
-      c = (uint64_t)k * P_RAW[i] + (c >> 32);
-      if ((uint32_t)i == word) w = (uint32_t)c;
-    }
-    g_kp_tab[j] = w;
-  }
-  __syncthreads();
-}
-struct KpLds {
-  DI u12 operator()(uint32_t q) const {
-    q = q < 10u ? q : 10u;  // q <= 10 by the operand bounds; the clamp keeps the read in the table
-    const uint4* r = reinterpret_cast<const uint4*>(g_kp_tab) + 3u * q;
-    const uint4 a = r[0], b = r[1], c = r[2];
-    u12 w;
-    w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w, w[4] = b.x, w[5] = b.y;
-    w[6] = b.z, w[7] = b.w, w[8] = c.x, w[9] = c.y, w[10] = c.z, w[11] = c.w;
-    return w;
-  }
-};
+// the reduction multiple of the fused 3u +- 2x (tower.h fp2_3u_pm_2x, q <= 10) from an LDS table of
+// k p, k < 11 (528 bytes per workgroup, tower.h kp_lds_init / KpLdsK; k_fexp_tri writes it)
+using KpLds = KpLdsK<11>;
 
 DI fp4 tri_cyclotomic_sqr(const tri_lane& t, const fp4& x_in) {
 #if BLS_CSQR_PARK
