@@ -8,7 +8,7 @@
 #   tests:EXPR       pytest -m gpu -k EXPR
 #   smoke            __graft_entry__.smoke() (no torch in the process) + the plain-C ABI harness
 #   bench            default bench.py (configs[1], cpu_baseline)
-#   fuzz10           tests/test_gpu_fuzz.py with DRAND_AMD_FUZZ_SCALE=10 (ten times the random cases)
+#   fuzz10, fuzz:N   tests/test_gpu_fuzz.py with DRAND_AMD_FUZZ_SCALE=10 / N (that many times the random cases)
 #   bench2           bench.py --gpus 2 --dist-backend gloo, weak and strong (two ranks on one GPU)
 #   prof             rocprofv3 --kernel-trace --stats of bench.py with BLSV_SERIAL_STAGES=1
 #   pmc              PMC passes: FETCH_SIZE, WRITE_SIZE, two SQ/GRBM sets (tools/pmc_sq.py)
@@ -43,9 +43,10 @@ for step in "$@"; do
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || rc=11 ;;
     bench) timeout -k 10 400 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" || rc=13 ;;
-    fuzz10)
-      DRAND_AMD_FUZZ_SCALE=10 timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py -x -v -m gpu -s \
-        --timeout 600 --timeout-method thread > "$O/pytest_gpu_fuzz_x10.log" 2>&1 || rc=16 ;;
+    fuzz10|fuzz:*)
+      F=10; [ "$step" != fuzz10 ] && F=${step#fuzz:}
+      DRAND_AMD_FUZZ_SCALE=$F timeout -k 10 1100 python -u -m pytest tests/test_gpu_fuzz.py -x -v -m gpu -s \
+        --timeout 1000 --timeout-method thread > "$O/pytest_gpu_fuzz_x$F.log" 2>&1 || rc=16 ;;
     bench2)
       timeout -k 10 300 python -u bench.py --gpus 2 --dist-backend gloo --n 262144 --steps 2 --warmup 1 \
         --cpu-per-worker 0 > "$O/bench2_weak.json" 2> "$O/bench2_weak.err" &&
